@@ -1,0 +1,163 @@
+"""Headline benchmark: BASELINE.json configs[1] -- 20-node discrete chain, d=32,
+65 536 batched queries per GPU through ``BayesianNetwork.infer`` (the
+reference's batched factor-product / mean-out / max-normalise loop,
+bayesian_network.py:208-305) on the HIP engine.
+
+One step = one ``infer`` call over one batch of 65 536 queries whose evidence
+columns are already resident in HBM (target X19, evidence on X0..X18 -- the
+reference's own benchmarking_df usage, every non-target column observed).
+Each step rebuilds the factor tables on the device; only host metadata (plan
+descriptors) is reused.  N > 1: the batch grows with N (weak scaling), each rank
+owns 65 536 queries and the ranks exchange the global max with one RCCL
+all-reduce between the two query passes (distributed.sharded_infer).
+
+Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` for the dominant
+kernel (the write pass) from HIP events in the timed region, and
+``cpu_baseline`` = the CPU oracle (a restatement of the reference algorithm,
+oracle/ref_infer.py) timed on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from continuousbayesiannetwork_amd import BayesianNetwork  # noqa: E402
+from continuousbayesiannetwork_amd.distributed import sharded_infer  # noqa: E402
+from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--queries", type=int, default=65536, help="queries per GPU")
+    ap.add_argument("--nodes", type=int, default=20)
+    ap.add_argument("--card", type=int, default=32)
+    ap.add_argument("--train-rows", type=int, default=200_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU oracle sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(data, cols, edges, ev_np, target, N, budget_s):
+    from oracle.ref_infer import OracleBN
+
+    ora = OracleBN(edges, cols, data)
+    q = 64
+    t = 0.0
+    while True:
+        sub = {k: v[:q] for k, v in ev_np.items()}
+        t0 = time.perf_counter()
+        ora.infer(target, sub, N)
+        t = time.perf_counter() - t0
+        if t > budget_s / 4 or q >= 65536:
+            break
+        q = min(65536, int(q * max(2.0, min(8.0, (budget_s / 4) / max(t, 1e-3)))))
+    return dict(value=q / t, unit="queries/s", cores=1, kind="port",
+                sample=f"oracle/ref_infer.py OracleBN.infer on the first {q} of the same queries "
+                       f"(numpy, 1 thread; {t:.2f} s)")
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    n, d, Q = a.nodes, a.card, a.queries
+    target = f"X{n - 1}"
+    data, cols, edges = chain_data(n, d, a.train_rows, 3, noise=(0.4, 0.25, 0.15, 0.1, 0.05, 0.05))
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
+    names = [c for c in cols if c != target]
+    ev_np = sample_evidence(data, cols, names, Q, seed=1000 + rank)
+    ev = {k: torch.tensor(v, device=dev) for k, v in ev_np.items()}
+
+    def step():
+        if world > 1:
+            return sharded_infer(bn, target, ev, N_max=d)
+        return bn.infer(target, ev, N_max=d)
+
+    random.seed(0)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    K = a.steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+            torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        bn.engine.timing_events = evs[i] if world == 1 else None
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    bn.engine.timing_events = None
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    sec = float(dt.item())
+    ms_per_step = sec / K * 1e3
+    value = Q * world * K / sec
+
+    roofline = None
+    if world == 1:
+        tmax = np.mean([e0.elapsed_time(e1) for e0, e1, _ in evs]) * 1e-3
+        twrite = np.mean([e1.elapsed_time(e2) for _, e1, e2 in evs]) * 1e-3
+        n_cols = len(names)  # evidence columns read by the write pass
+        bytes_write = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
+        achieved = bytes_write / twrite / 1e9
+        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                        kernel="k_query<4,LDS,write>", avg_us=round(twrite * 1e6, 2),
+                        algorithmic_bytes_per_launch=bytes_write,
+                        max_pass_us=round(tmax * 1e6, 2))
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(data, cols, edges, ev_np, target, d, a.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "marginal queries/sec + achieved HBM GB/s, 20-node d=32 DAG, 65k-batch VE",
+            "value": round(value, 1), "unit": "queries/s", "n_gpus": world, "steps": K, "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded chain samples; BruteForce fit)",
+            "config": {"workload": f"chain{n}_d{d}: BayesianNetwork.infer target {target}, evidence on the other "
+                                   f"{n - 1} nodes, N_max={d}", "queries_per_gpu": Q, "global_batch": Q * world,
+                       "parallelism": f"query-shard x{world}" + (" + RCCL all-reduce(max)" if world > 1 else "")},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+"""ctypes binding of libcbn_amd.so (the C ABI declared in include/cbn_amd.h).
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7``
+dependency resolves to the HIP runtime torch already mapped (same SONAME):
+device pointers from torch's allocator and torch's streams are then valid
+inside the library.  There is no CPU fallback: if the library or a GPU is
+missing every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcbn_amd.so")
+
+CBN_MAX_PARENTS = 8
+CBN_MAX_EVIDENCE = 64
+CBN_FACTOR_SCALAR = 0
+CBN_FACTOR_SHARED = 1
+CBN_FACTOR_QUERY = 2
+
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_c_int_p = ctypes.POINTER(ctypes.c_int32)
+
+
+class FactorDesc(ctypes.Structure):
+    """Mirror of ``cbn_factor_desc`` (include/cbn_amd.h)."""
+
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("n_parents", ctypes.c_int32),
+        ("node_card", ctypes.c_int32),
+        ("parent_card", ctypes.c_int32 * CBN_MAX_PARENTS),
+        ("parent_ev_slot", ctypes.c_int32 * CBN_MAX_PARENTS),
+        ("cpd", ctypes.c_void_p),
+        ("node_sample_idx", ctypes.c_void_p),
+        ("parent_sample_idx", ctypes.c_void_p),
+        ("parent_domain", ctypes.c_void_p * CBN_MAX_PARENTS),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "cbn_abi_version": (ctypes.c_int, []),
+    "cbn_last_error": (ctypes.c_char_p, []),
+    "cbn_bf_cpd_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_bf_cpd_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_plan_create": (ctypes.c_int, [ctypes.POINTER(FactorDesc), ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "cbn_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbn_plan_table_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
+    "cbn_plan_uses_lds": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbn_plan_build_tables": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_plan_query_max": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_plan_query_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_plan_infer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(no CPU fallback exists for the HIP inference path)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.cbn_abi_version() != 1:
+            raise NativeError("libcbn_amd.so ABI version mismatch")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().cbn_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (rc={rc}): {msg}")
+
+
+def require_gpu(device) -> torch.device:
+    device = torch.device(device)
+    if device.type != "cuda" or not torch.cuda.is_available():
+        raise NativeError(
+            f"the MI355X inference path needs a HIP device, got device={device!s} "
+            f"(torch.cuda.is_available()={torch.cuda.is_available()})")
+    load()
+    return device
+
+
+def stream_ptr(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())

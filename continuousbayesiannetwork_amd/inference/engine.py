@@ -1,0 +1,288 @@
+"""Batched inference engine behind ``BayesianNetwork.infer``.
+
+Reference path (cbn/base/bayesian_network.py:208-305): for every ancestor of the
+target (topological order, target last) build the per-query pdf tensor
+``[n_queries, d_0..d_{k-1}, N]`` with Node.get_prob, average it over the
+parent axes, multiply the averages into ``out_pdf`` and divide by the global
+max.  This engine computes the same numbers in three launches:
+
+  1. ``k_build_tables``  -- every factor's mean over its unobserved parents as a
+     small table (indexed by the observed parents' domain indices),
+  2. ``k_query<max>``     -- per query/value product of the gathered table rows,
+     folded into the global max,
+  3. ``k_query<write>``   -- the same product divided by the max, written out.
+
+Host work per call is one dict walk and one C call; the plan (descriptors,
+sample-domain index arrays, device image) is cached per
+(target, observed parent columns, N_max) when every sample domain is
+deterministic (N_max <= |domain|).  When the reference would draw random
+padding values (node.py:302-333) the plan is rebuilt on every call, consuming
+Python's ``random`` in the reference's order, so results stay identical.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import _native
+from .._native import CBN_FACTOR_QUERY, CBN_FACTOR_SCALAR, CBN_FACTOR_SHARED, CBN_MAX_EVIDENCE, CBN_MAX_PARENTS
+
+
+def domain_index(values: torch.Tensor, domain: torch.Tensor) -> torch.Tensor:
+    """int32 index of each value in the sorted ``domain``; -1 when absent."""
+    values = values.to(device=domain.device, dtype=domain.dtype).contiguous()
+    i = torch.searchsorted(domain, values).clamp_(max=domain.numel() - 1)
+    return torch.where(domain[i] == values, i, torch.full_like(i, -1)).to(torch.int32)
+
+
+@dataclass
+class FactorSpec:
+    """Host-side description of one factor (also used by the CPU tests)."""
+    node: str
+    kind: int
+    parents: List[str]
+    observed: List[str]
+    free_samples: Dict[str, torch.Tensor]
+    node_samples: torch.Tensor
+
+
+@dataclass
+class Plan:
+    target: str
+    n_samples: int
+    order: List[str]
+    factors: List[FactorSpec]
+    slots: List[str]
+    target_domain: torch.Tensor
+    target_observed: bool
+    deterministic: bool
+    handle: Optional[ctypes.c_void_p] = None
+    keep: list = field(default_factory=list)
+    max_bits: Optional[torch.Tensor] = None
+
+    def destroy(self):
+        if self.handle is not None and self.handle.value:
+            _native.load().cbn_plan_destroy(self.handle)
+        self.handle = None
+        self.keep = []
+
+
+def relevant_observed(bn, order: Sequence[str], evidence_keys) -> frozenset:
+    keys = set(evidence_keys)
+    rel = set()
+    for n in order:
+        rel.update(p for p in bn.nodes_obj[n].parents_names if p in keys)
+    return frozenset(rel)
+
+
+def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[List[str], List[FactorSpec], torch.Tensor, bool]:
+    """Walk the factors in the reference's order, calling sample_domain exactly
+    where Node.get_prob / BayesianNetwork.infer do (node.py:243-256, 263-276,
+    :153-156; bayesian_network.py:265-267)."""
+    order = bn.get_ancestors(bn.initial_dag, target)
+    order.append(target)
+    specs = []
+    deterministic = True
+    target_dom = None
+    for n in order:
+        nd = bn.nodes_obj[n]
+        parents = list(nd.parents_names)
+        obs = [p for p in parents if p in observed]
+        free = [p for p in parents if p not in obs] if (parents and obs != parents) else []
+        free_samples = {}
+        for p in parents:
+            if p in free:
+                deterministic &= nd.sample_domain_is_deterministic(nd.info[p], N)
+                free_samples[p] = nd.sample_domain(p, N)
+        deterministic &= nd.sample_domain_is_deterministic(nd.info[n], N)
+        node_samples = nd.sample_domain(n, N)
+        kind = CBN_FACTOR_SCALAR if not parents else (CBN_FACTOR_QUERY if obs else CBN_FACTOR_SHARED)
+        specs.append(FactorSpec(n, kind, parents, obs, free_samples, node_samples))
+        if n == target:
+            target_dom = node_samples
+    # bayesian_network.py:265-267 draws the target domain once more (shape only)
+    bn.nodes_obj[target].sample_domain(target, N)
+    return order, specs, target_dom, deterministic
+
+
+class InferenceEngine:
+    def __init__(self, bn):
+        self.bn = bn
+        self._plans: Dict[tuple, Plan] = {}
+        self._orders: Dict[str, List[str]] = {}
+        # optional (start, mid, end) torch.cuda.Event triple recorded around the
+        # max / write passes of the next calls (bench.py's per-kernel timing)
+        self.timing_events = None
+
+    def invalidate(self):
+        if self._plans:
+            torch.cuda.synchronize()
+        for p in self._plans.values():
+            p.destroy()
+        self._plans = {}
+        self._orders = {}
+
+    def __del__(self):
+        try:
+            for p in self._plans.values():
+                p.destroy()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- plan --
+    def _materialise(self, plan: Plan, device: torch.device):
+        lib = _native.load()
+        descs = (_native.FactorDesc * len(plan.factors))()
+        keep = []
+        slot_of = {v: i for i, v in enumerate(plan.slots)}
+        N = plan.n_samples
+        with torch.cuda.device(device):
+            for f, spec in enumerate(plan.factors):
+                est = self.bn.nodes_obj[spec.node].estimator
+                cpd = est.compiled()
+                doms = est.domains
+                d = descs[f]
+                d.kind = spec.kind
+                d.n_parents = len(spec.parents)
+                if d.n_parents > CBN_MAX_PARENTS:
+                    raise _native.NativeError(f"node {spec.node}: {d.n_parents} parents > {CBN_MAX_PARENTS}")
+                d.node_card = int(doms[-1].numel())
+                d.cpd = cpd.data_ptr() if spec.kind != CBN_FACTOR_SCALAR else est.node_marginal.data_ptr()
+                nidx = domain_index(spec.node_samples, doms[-1])
+                keep.append(nidx)
+                d.node_sample_idx = nidx.data_ptr()
+                if spec.parents:
+                    pidx = torch.zeros((len(spec.parents), N), dtype=torch.int32, device=device)
+                    for i, p in enumerate(spec.parents):
+                        if p in spec.free_samples:
+                            pidx[i] = domain_index(spec.free_samples[p], doms[i])
+                    keep.append(pidx)
+                    d.parent_sample_idx = pidx.data_ptr()
+                for i, p in enumerate(spec.parents):
+                    d.parent_card[i] = int(doms[i].numel())
+                    if p in spec.observed:
+                        d.parent_ev_slot[i] = slot_of[p]
+                        d.parent_domain[i] = doms[i].data_ptr()
+                    else:
+                        d.parent_ev_slot[i] = -1
+            handle = ctypes.c_void_p()
+            torch.cuda.current_stream(device).synchronize()  # index arrays ready before the D2D copies
+            _native.check(lib.cbn_plan_create(descs, len(plan.factors), N, ctypes.byref(handle)),
+                          "cbn_plan_create")
+        plan.handle = handle
+        plan.keep = keep
+        plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def plan(self, target: str, observed: frozenset, N: int, device) -> Plan:
+        key = (target, observed, int(N))
+        p = self._plans.get(key)
+        if p is not None:
+            return p
+        order, specs, tdom, det = build_factor_specs(self.bn, target, observed, N)
+        slots = sorted({o for s in specs for o in s.observed})
+        if len(slots) > CBN_MAX_EVIDENCE:
+            raise _native.NativeError(f"{len(slots)} observed columns > {CBN_MAX_EVIDENCE}")
+        tobs = any(s.observed for s in specs if s.node == target)
+        p = Plan(target, int(N), order, specs, slots, tdom, tobs, det)
+        self._materialise(p, device)
+        if det:
+            self._plans[key] = p
+        return p
+
+    # --------------------------------------------------------------- infer --
+    def _order(self, target: str) -> List[str]:
+        order = self._orders.get(target)
+        if order is None:
+            order = self._orders[target] = self.bn.get_ancestors(self.bn.initial_dag, target) + [target]
+        return order
+
+    def _columns(self, plan: Plan, evidence, n_queries: int, device) -> List[torch.Tensor]:
+        cols = []
+        for v in plan.slots:
+            t = evidence[v]
+            assert t.dim() == 2, ValueError("Each query tensor must be of dimension 2.")
+            assert t.shape[0] == n_queries, ValueError("n_queries must be equal for all features.")
+            if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(device=device, dtype=torch.float32).contiguous()
+            cols.append(t)
+        return cols
+
+    def prepare(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int):
+        """Plan + device evidence columns of one (deterministic) call, without launching."""
+        device = _native.require_gpu(self.bn.device)
+        evidence.items()
+        n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
+        observed = relevant_observed(self.bn, self._order(target), evidence.keys())
+        plan = self.plan(target, observed, N_max, device)
+        if not plan.deterministic:
+            plan.destroy()
+            raise NotImplementedError(
+                "sharded inference needs N_max <= |domain| for every sampled variable: the reference pads "
+                "larger domains with per-call random values (node.py:302-333) that ranks cannot share")
+        cols = self._columns(plan, evidence, n_queries, device)
+        tq = n_queries if plan.target_observed else 1
+        return plan, cols, n_queries, plan.target_domain.unsqueeze(0).expand(tq, -1), device
+
+    def infer(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int,
+              out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        device = _native.require_gpu(self.bn.device)
+        items = evidence.items()  # evidence=None raises here, as bayesian_network.py:193 does
+        n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
+        observed = relevant_observed(self.bn, self._order(target), evidence.keys())
+        plan = self.plan(target, observed, N_max, device)
+        try:
+            return self._run(plan, dict(items), n_queries, device, out)
+        finally:
+            if not plan.deterministic:
+                torch.cuda.current_stream(device).synchronize()
+                plan.destroy()
+
+    def _run(self, plan: Plan, evidence, n_queries: int, device, out):
+        lib = _native.load()
+        N = plan.n_samples
+        cols = self._columns(plan, evidence, n_queries, device)
+        tq = n_queries if plan.target_observed else 1
+        tdom = plan.target_domain.unsqueeze(0).expand(tq, -1)
+        if (n_queries, N) != tuple(tdom.shape):
+            raise AssertionError("pdf and domain must have same shape.")
+        if n_queries == 0:
+            raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")
+        if out is None:
+            out = torch.empty((n_queries, N), dtype=torch.float32, device=device)
+        if self.timing_events is not None:
+            e0, e1, e2 = self.timing_events
+            e0.record()
+            self.query_max(plan, cols, n_queries, device)
+            e1.record()
+            self.query_write(plan, cols, n_queries, plan.max_bits, out, device)
+            e2.record()
+            return out, tdom
+        ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        with torch.cuda.device(device):
+            _native.check(lib.cbn_plan_infer(plan.handle, n_queries, ptrs, len(cols),
+                                             _native.ptr(plan.max_bits), _native.ptr(out),
+                                             _native.stream_ptr(device)), "cbn_plan_infer")
+        return out, tdom
+
+    # ---------------------------------------------- split passes (sharded) --
+    def query_max(self, plan: Plan, cols: List[torch.Tensor], n_queries: int, device) -> torch.Tensor:
+        lib = _native.load()
+        ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        with torch.cuda.device(device):
+            s = _native.stream_ptr(device)
+            _native.check(lib.cbn_plan_build_tables(plan.handle, _native.ptr(plan.max_bits), s), "build_tables")
+            _native.check(lib.cbn_plan_query_max(plan.handle, n_queries, ptrs, len(cols),
+                                                 _native.ptr(plan.max_bits), s), "query_max")
+        return plan.max_bits
+
+    def query_write(self, plan: Plan, cols: List[torch.Tensor], n_queries: int, max_bits: torch.Tensor,
+                    out: torch.Tensor, device):
+        lib = _native.load()
+        ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        with torch.cuda.device(device):
+            _native.check(lib.cbn_plan_query_write(plan.handle, n_queries, ptrs, len(cols), _native.ptr(max_bits),
+                                                   _native.ptr(out), _native.stream_ptr(device)), "query_write")
+        return out

@@ -1,0 +1,119 @@
+/*
+ * cbn_amd.h -- C ABI of the MI355X-native batched inference engine for
+ * ContinuousBayesianNetwork (libcbn_amd.so).
+ *
+ * Plain C: pointers, sizes, int32/int64/float; device pointers are HIP device
+ * addresses; `stream` is a hipStream_t passed as void* (NULL = default stream).
+ * No torch types cross this boundary.  Every entry point returns 0 on success
+ * and a negative CBN_E* code on failure; cbn_last_error() gives the message.
+ *
+ * Each entry point names the reference interface it replaces
+ * (Giovannibriglia/ContinuousBayesianNetwork, file:line).
+ */
+#ifndef CBN_AMD_H
+#define CBN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBN_AMD_ABI_VERSION 1
+
+#define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
+#define CBN_MAX_EVIDENCE 64  /* distinct evidence columns per query batch        */
+
+#define CBN_OK 0
+#define CBN_E_ARG -1
+#define CBN_E_HIP -2
+#define CBN_E_LIMIT -3
+
+/* Factor kinds of bayesian_network.py:271-294 (the per-node `x` multiplied
+ * into out_pdf):
+ *   SCALAR : root node, pdf [1, N]      -> x = mean over the N samples     [1]
+ *   SHARED : parents, none observed     -> x = mean over N^k parent combos [1, N]
+ *   QUERY  : >=1 parent observed        -> x = mean over free-parent combos,
+ *            indexed per query by the observed parents' values          [Q, N] */
+#define CBN_FACTOR_SCALAR 0
+#define CBN_FACTOR_SHARED 1
+#define CBN_FACTOR_QUERY 2
+
+/* One node's factor on the inference path of BayesianNetwork.infer
+ * (bayesian_network.py:241-255 builds one `pdfs` per ancestor via
+ * Node.get_prob, node.py:115-204).  All pointers are device pointers. */
+typedef struct cbn_factor_desc {
+    int32_t kind;                                 /* CBN_FACTOR_*                        */
+    int32_t n_parents;                            /* k (sorted parent order, node.py:65) */
+    int32_t node_card;                            /* |domain(node)|                      */
+    int32_t parent_card[CBN_MAX_PARENTS];         /* |domain(parent_i)|                  */
+    int32_t parent_ev_slot[CBN_MAX_PARENTS];      /* -1: free parent; else evidence col  */
+    const float* cpd;                             /* dense CPD [parent_card..., node_card]
+                                                     (root: marginal [node_card])        */
+    const int32_t* node_sample_idx;               /* [N] node sample -> domain idx or -1 */
+    const int32_t* parent_sample_idx;             /* [k*N] free-parent sample idx or -1  */
+    const float* parent_domain[CBN_MAX_PARENTS];  /* sorted domain values (observed parents) */
+} cbn_factor_desc;
+
+typedef struct cbn_plan cbn_plan;  /* opaque: device descriptors + factor tables */
+
+/* ABI version / last error message of the calling thread. */
+int cbn_abi_version(void);
+const char* cbn_last_error(void);
+
+/* Dense BruteForce CPD from the fitted maximum-likelihood rows.
+ * Replaces brute_force.py:30-66 (_fit's mle_tensor) + the per-call equality
+ * scans of brute_force.py:240-254 (joint / parent-marginal sums).
+ *   cell[r]  : flat index of mle row r in [n_parent_cells, node_card]
+ *   prob[r]  : its empirical probability (counts / total)
+ *   normalize: 1 -> cpd = joint / (sum_v joint + 1e-10)  (conditional, :253)
+ *              0 -> cpd = joint                          (root marginal, :205-214) */
+int cbn_bf_cpd_build(const int32_t* cell, const float* prob, int64_t n_rows,
+                     int64_t n_parent_cells, int32_t node_card, int32_t normalize,
+                     float* cpd, void* stream);
+
+/* Evaluate a dense BruteForce CPD at arbitrary float points.
+ * Replaces BruteForce._get_prob (brute_force.py:185-257):
+ *   points   : [n_points, n_cols] float32, columns = parents..., node
+ *   domains  : per column, a sorted domain array (device) and its size
+ *   out[i]   : cpd[idx(points[i])], 0 where any value is not in its domain
+ *              (the reference's 0 / (0 + 1e-10)). */
+int cbn_bf_cpd_eval(const float* cpd, int32_t n_cols, const float* const* domains,
+                    const int32_t* domain_card, const float* points, int64_t n_points,
+                    float* out, void* stream);
+
+/* Build a plan for one (target node, observed-column set, N_max) of
+ * BayesianNetwork.infer (bayesian_network.py:208-305).  Copies the
+ * descriptors to the device and allocates the factor tables. */
+int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n_samples,
+                    cbn_plan** plan);
+int cbn_plan_destroy(cbn_plan* plan);
+/* Bytes of factor tables / whether the query kernels stage them in LDS. */
+int64_t cbn_plan_table_bytes(const cbn_plan* plan);
+int cbn_plan_uses_lds(const cbn_plan* plan);
+
+/* Marginalise the free parents of every factor into its table
+ * (the torch.mean(pdf, dim=parent dims) of bayesian_network.py:292) and zero
+ * *max_bits.  One launch for all factors. */
+int cbn_plan_build_tables(cbn_plan* plan, uint32_t* max_bits, void* stream);
+
+/* Pass 1: atomically fold max over (q, j) of prod_f x_f[q, j] into *max_bits
+ * (float bits; all values are >= 0).  evidence[c] is the [n_queries] float32
+ * column for evidence slot c (node.py:230-256 reads them as float32). */
+int cbn_plan_query_max(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
+                       int32_t n_evidence, uint32_t* max_bits, void* stream);
+
+/* Pass 2: out[q, j] = prod_f x_f[q, j] / max  (bayesian_network.py:269-296),
+ * out is [n_queries, N] row-major float32. */
+int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
+                         int32_t n_evidence, const uint32_t* max_bits, float* out,
+                         void* stream);
+
+/* build_tables + query_max + query_write on one stream (single GPU). */
+int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
+                   int32_t n_evidence, uint32_t* max_bits, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CBN_AMD_H */

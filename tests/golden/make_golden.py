@@ -1,0 +1,182 @@
+"""Generate golden input/output vectors by running the REFERENCE itself.
+
+Run here (the container that has /root/reference), never on the GPU box:
+
+    python tests/golden/make_golden.py
+
+It imports the reference's own modules from /root/reference and calls
+``BayesianNetwork.infer`` (cbn/base/bayesian_network.py:208-305) on small
+seeded networks fitted with the BruteForce estimator
+(cbn/parameter_learning/brute_force.py).  The reference package's
+``cbn/parameter_learning/__init__.py`` imports the GP estimator, whose
+third-party dependency (gpytorch ~=1.14, requirements.txt) is not installed in
+this image; the package is therefore assembled from the reference's own
+brute_force.py module without executing that ``__init__`` (the GP estimator is
+not on the inference path).  No reference source is copied: only the
+inputs/outputs land in ``tests/golden/*.npz``.
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+
+def _load_reference():
+    sys.path.insert(0, REF)
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[name] = m
+        spec.loader.exec_module(m)
+        return m
+
+    import cbn  # noqa: F401  (empty package __init__)
+
+    pl = types.ModuleType("cbn.parameter_learning")
+    pl.__path__ = [REF + "/cbn/parameter_learning"]
+    sys.modules["cbn.parameter_learning"] = pl
+    bf = load("cbn.parameter_learning.brute_force", REF + "/cbn/parameter_learning/brute_force.py")
+    pl.ESTIMATORS = {"brute_force": bf.BruteForce}
+    from cbn.base.bayesian_network import BayesianNetwork
+
+    return BayesianNetwork
+
+
+# ----------------------------------------------------------------- data -----
+def chain_data(n, d, S, seed, values=None):
+    rng = np.random.default_rng(seed)
+    X = np.zeros((S, n), np.int64)
+    X[:, 0] = rng.integers(0, d, S)
+    for i in range(1, n):
+        X[:, i] = (X[:, i - 1] + rng.choice(3, S, p=[0.6, 0.3, 0.1])) % d
+    vals = np.arange(d, dtype=np.float32) if values is None else np.asarray(values, np.float32)
+    cols = [f"X{i}" for i in range(n)]
+    edges = [(f"X{i}", f"X{i+1}") for i in range(n - 1)]
+    return vals[X], cols, edges
+
+
+def multi_data(S, seed):
+    """A, B -> C ; C, D -> E ; A -> D ; d = 3 with non-integer values."""
+    rng = np.random.default_rng(seed)
+    A = rng.integers(0, 3, S)
+    B = rng.integers(0, 3, S)
+    C = (A + B + rng.integers(0, 2, S)) % 3
+    D = (A + rng.choice(3, S, p=[0.7, 0.2, 0.1])) % 3
+    E = (C * D + rng.integers(0, 2, S)) % 3
+    vals = np.array([-1.5, 0.25, 2.0], np.float32)
+    X = np.stack([A, B, C, D, E], 1)
+    cols = ["A", "B", "C", "D", "E"]
+    edges = [("A", "C"), ("B", "C"), ("C", "E"), ("D", "E"), ("A", "D")]
+    return vals[X], cols, edges
+
+
+def sample_evidence(data, cols, names, Q, seed, missing_frac=0.0, missing_value=7.5):
+    rng = np.random.default_rng(seed)
+    rows = rng.integers(0, data.shape[0], Q)
+    ev = {}
+    for nm in names:
+        v = data[rows, cols.index(nm)].astype(np.float32).reshape(Q, 1)
+        if missing_frac > 0:
+            m = rng.random(Q) < missing_frac
+            v[m, 0] = missing_value
+        ev[nm] = v
+    return ev
+
+
+CASES = [
+    # name, data-fn, target, evidence names, Q, N_max, rnd seed, extra
+    dict(name="chain5_d4_q1024_parent", data=("chain", 5, 4, 3000, 1), target="X4",
+         ev=["X3"], Q=1024, N=4),
+    dict(name="chain5_d4_all_evidence", data=("chain", 5, 4, 3000, 2), target="X4",
+         ev=["X0", "X1", "X2", "X3"], Q=64, N=4),
+    dict(name="chain5_d4_noevidence", data=("chain", 5, 4, 3000, 3), target="X4",
+         ev=[], Q=1, N=4),
+    dict(name="chain5_d4_subsample", data=("chain", 5, 4, 3000, 4), target="X4",
+         ev=["X3", "X1"], Q=32, N=3),
+    dict(name="chain5_d4_oversample", data=("chain", 5, 4, 3000, 5), target="X4",
+         ev=["X3"], Q=16, N=6, seed=123),
+    dict(name="chain6_d5_float_values", data=("chain", 6, 5, 4000, 6, [0.1, 0.7, 1.3, 2.9, 11.0]),
+         target="X5", ev=["X4", "X2"], Q=48, N=5),
+    dict(name="multi_partial", data=("multi", 2000, 7), target="E",
+         ev=["C", "A"], Q=20, N=3),
+    dict(name="multi_all_parents", data=("multi", 2000, 8), target="E",
+         ev=["C", "D", "A", "B"], Q=40, N=3),
+    dict(name="multi_missing_values", data=("multi", 2000, 9), target="E",
+         ev=["C", "D"], Q=40, N=3, missing=0.25),
+    dict(name="multi_target_C_oversample", data=("multi", 2000, 10), target="C",
+         ev=["A", "B"], Q=12, N=5, seed=7),
+    dict(name="root_target_q1", data=("chain", 4, 3, 500, 11), target="X0",
+         ev=[], Q=1, N=3),
+    dict(name="err_evidence_none", data=("chain", 4, 3, 500, 13), target="X3",
+         ev=[], Q=1, N=3, evidence_none=True, expect_error=True),
+    dict(name="err_target_parent_free", data=("chain", 5, 4, 500, 12), target="X4",
+         ev=["X1"], Q=8, N=4, expect_error=True),
+]
+
+
+def make_data(spec):
+    if spec[0] == "chain":
+        vals = spec[5] if len(spec) > 5 else None
+        return chain_data(spec[1], spec[2], spec[3], spec[4], vals)
+    return multi_data(spec[1], spec[2])
+
+
+def main():
+    import networkx as nx
+    import pandas as pd
+    import torch
+
+    BayesianNetwork = _load_reference()
+    manifest = []
+    for c in CASES:
+        data, cols, edges = make_data(c["data"])
+        dag = nx.DiGraph()
+        dag.add_nodes_from(cols)
+        dag.add_edges_from(edges)
+        df = pd.DataFrame(data, columns=cols)
+        bn = BayesianNetwork(dag, df, {"estimator_name": "brute_force"},
+                             {"inference_obj": "exact"}, device="cpu")
+        ev = sample_evidence(data, cols, c["ev"], c["Q"], seed=100 + len(manifest),
+                             missing_frac=c.get("missing", 0.0))
+        ev_t = {k: torch.tensor(v) for k, v in ev.items()}
+        if c.get("evidence_none"):
+            ev_t = None
+        seed = c.get("seed", 0)
+        random.seed(seed)
+        err = ""
+        pdf = dom = np.zeros((0,), np.float32)
+        try:
+            p, d = bn.infer(c["target"], ev_t, N_max=c["N"])
+            pdf, dom = p.numpy().astype(np.float32), d.numpy().astype(np.float32)
+        except AssertionError as e:  # reference's shape assertion (bayesian_network.py:301)
+            err = "AssertionError:" + str(e)
+        except AttributeError as e:  # evidence=None (bayesian_network.py:193)
+            err = "AttributeError:" + str(e)
+        assert bool(err) == bool(c.get("expect_error", False)), (c["name"], err)
+        out = dict(data=data.astype(np.float32), pdf=pdf, domain=dom,
+                   meta=np.array(json.dumps(dict(
+                       name=c["name"], columns=cols, edges=edges, target=c["target"],
+                       evidence=list(ev.keys()), evidence_none=bool(c.get("evidence_none")), N_max=c["N"], seed=seed, error=err))))
+        for k, v in ev.items():
+            out["ev_" + k] = v
+        np.savez_compressed(os.path.join(HERE, c["name"] + ".npz"), **out)
+        manifest.append(c["name"])
+        print(c["name"], pdf.shape, err)
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump(dict(generator="tests/golden/make_golden.py",
+                       reference="Giovannibriglia/ContinuousBayesianNetwork @ /root/reference",
+                       cases=manifest), f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

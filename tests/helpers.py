@@ -1,0 +1,56 @@
+"""Builders shared by the CPU and GPU tests (synthetic data; no reference import)."""
+import networkx as nx
+import numpy as np
+import pandas as pd
+
+
+def make_bn(cls, edges, columns, data, device, estimator="brute_force"):
+    dag = nx.DiGraph()
+    dag.add_nodes_from(columns)
+    dag.add_edges_from(edges)
+    df = pd.DataFrame(data, columns=columns)
+    return cls(dag, df, {"estimator_name": estimator}, {"inference_obj": "exact"}, device=device)
+
+
+def chain_data(n, d, S, seed, values=None, noise=(0.6, 0.3, 0.1)):
+    rng = np.random.default_rng(seed)
+    X = np.zeros((S, n), np.int64)
+    X[:, 0] = rng.integers(0, d, S)
+    for i in range(1, n):
+        X[:, i] = (X[:, i - 1] + rng.choice(len(noise), S, p=list(noise))) % d
+    vals = np.arange(d, dtype=np.float32) if values is None else np.asarray(values, np.float32)
+    cols = [f"X{i}" for i in range(n)]
+    edges = [(f"X{i}", f"X{i+1}") for i in range(n - 1)]
+    return vals[X], cols, edges
+
+
+def random_dag_data(n, d, max_parents, S, seed):
+    """Random DAG over X0..X{n-1} (edges only from lower to higher index)."""
+    rng = np.random.default_rng(seed)
+    edges = []
+    X = np.zeros((S, n), np.int64)
+    for i in range(n):
+        k = int(rng.integers(0, min(i, max_parents) + 1))
+        if i == n - 1:
+            k = max(k, 1)
+        ps = sorted(rng.choice(i, size=k, replace=False).tolist()) if k else []
+        edges += [(f"X{p}", f"X{i}") for p in ps]
+        base = rng.integers(0, d, S)
+        for p in ps:
+            base = base + X[:, p] * int(rng.integers(1, 3))
+        X[:, i] = (base + rng.integers(0, 2, S)) % d
+    cols = [f"X{i}" for i in range(n)]
+    return X.astype(np.float32), cols, edges
+
+
+def sample_evidence(data, cols, names, Q, seed, missing_frac=0.0, missing_value=7.5):
+    rng = np.random.default_rng(seed)
+    rows = rng.integers(0, data.shape[0], Q)
+    ev = {}
+    for nm in names:
+        v = data[rows, cols.index(nm)].astype(np.float32).reshape(Q, 1)
+        if missing_frac > 0:
+            m = rng.random(Q) < missing_frac
+            v[m, 0] = missing_value
+        ev[nm] = v
+    return ev

@@ -1,0 +1,39 @@
+"""The C ABI library loads and exports every entry point include/cbn_amd.h declares
+(no compute: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+from continuousbayesiannetwork_amd import _native
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "cbn_amd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cbn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_native.EXPORTED_SYMBOLS)
+
+
+def test_abi_version_and_struct_layout():
+    lib = _native.load()
+    assert lib.cbn_abi_version() == 1
+    # cbn_factor_desc: 3 int32 + 2*8 int32 + 3 pointers + 8 pointers (with alignment padding)
+    assert ctypes.sizeof(_native.FactorDesc) == 4 * 19 + 4 + 8 * 11
+
+
+def test_argument_errors_are_reported_without_gpu():
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    rc = lib.cbn_plan_create(None, 0, 4, ctypes.byref(h))
+    assert rc == -1
+    assert b"bad arguments" in lib.cbn_last_error()

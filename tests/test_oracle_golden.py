@@ -1,0 +1,40 @@
+"""The CPU oracle (oracle/ref_infer.py) against vectors produced by running the
+reference itself (tests/golden/make_golden.py).  Tolerance: the oracle and the
+reference sum the parent-axis means in different orders, so rtol 1e-5 (the
+north-star fp32 bar) with atol 1e-7."""
+import random
+
+import numpy as np
+import pytest
+
+from golden_io import golden_names, load_golden
+from oracle.ref_infer import OracleBN
+
+RTOL, ATOL = 1e-5, 1e-7
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_oracle_matches_reference_golden(name):
+    g = load_golden(name)
+    m = g["meta"]
+    bn = OracleBN(m["edges"], m["columns"], g["data"])
+    random.seed(m["seed"])
+    ev = None if m["evidence_none"] else {k: g["evidence"][k] for k in m["evidence"]}
+    if m["error"]:
+        exc = AttributeError if m["error"].startswith("AttributeError") else AssertionError
+        with pytest.raises(exc):
+            if ev is None:
+                ev.items()
+            bn.infer(m["target"], ev, m["N_max"])
+        return
+    pdf, dom = bn.infer(m["target"], ev, m["N_max"])
+    assert pdf.shape == g["pdf"].shape
+    np.testing.assert_array_equal(dom, g["domain"])
+    np.testing.assert_allclose(pdf, g["pdf"], rtol=RTOL, atol=ATOL)
+
+
+def test_golden_manifest_covers_config0():
+    """BASELINE configs[0]: 5-node chain, d=4, 1024 queries on the reference CPU path."""
+    g = load_golden("chain5_d4_q1024_parent")
+    assert g["pdf"].shape == (1024, 4)
+    assert len(g["meta"]["columns"]) == 5
