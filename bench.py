@@ -86,7 +86,7 @@ def main():
 
     n, d, Q = a.nodes, a.card, a.queries
     target = f"X{n - 1}"
-    data, cols, edges = chain_data(n, d, a.train_rows, 3, noise=(0.4, 0.25, 0.15, 0.1, 0.05, 0.05))
+    data, cols, edges = chain_data(n, d, a.train_rows, 3, stay=0.8)
     bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
     names = [c for c in cols if c != target]
     ev_np = sample_evidence(data, cols, names, Q, seed=1000 + rank)

@@ -55,7 +55,7 @@ _SIGNATURES = {
     "cbn_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "cbn_plan_table_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_uses_lds": (ctypes.c_int, [ctypes.c_void_p]),
-    "cbn_plan_build_tables": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_plan_build_tables": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "cbn_plan_query_max": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                           ctypes.c_void_p, ctypes.c_void_p]),
     "cbn_plan_query_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,

@@ -59,7 +59,6 @@ constexpr int kWave = 64;
 constexpr int kQueryThreads = 1024;
 constexpr int kBuildThreads = 256;
 constexpr int kLdsBudget = 160 * 1024;
-constexpr int kReduceLds = (kQueryThreads / kWave) * sizeof(float);
 
 // Device-side factor descriptor (built once per plan, read with wave-uniform
 // indices so the compiler keeps it on the scalar path).
@@ -71,17 +70,15 @@ struct DevFactor {
     int parent_card[kMaxP];
     int ev_slot[kMaxP];
     int cpd_stride[kMaxP];
-    int dom_off[kMaxP];        // float offset of observed parent's domain in the image
     const float* cpd;
     const int* node_sample_idx;
     const int* parent_sample_idx;
-    long long table_off;       // float offset of this factor's table in the image
-    long long rows;            // prod(card of observed parents) (QUERY) or 1
-    long long n_entries;       // table entries
-    long long free_combos;     // N^n_free
-    int wave_mode;             // 1: one wave per entry (many free combos)
-    long long unit_begin;      // prefix of work units over factors
-    long long n_units;
+    int table_off;   // float offset of this factor's table ([rows][N]) in the image
+    int rows;        // prod(card of observed parents) (QUERY) or 1
+    int n_entries;   // rows * N
+    int free_combos; // N^n_free
+    int wave_mode;   // build kernel: 1 = one wave per entry (many free combos)
+    int fill;        // LDS fill: 0 pre-built, 1 CPD rows, 2 CPD gather, 3 root mean
 };
 
 struct EvPtrs {
@@ -150,47 +147,47 @@ __global__ void k_cpd_eval(const float* __restrict__ cpd, int n_cols, ColPtrs co
 }
 
 // --------------------------------------------------------------- tables ----
-// Value of one table entry restricted to the free-combo range [c0, c1) with
-// step `cs`.  Table entry = (1/F) sum_{free combos} cpd[observed idx, free
-// sample idx, node sample idx]; samples not in the domain contribute 0 but
-// still count in F (node.py:291-333 pads with off-domain values).
-__device__ float entry_partial(const DevFactor& d, long long entry, int N, long long c0,
-                               long long c1, long long cs) {
+// Table entry = (1/F) sum over free-parent sample combos of
+// cpd[observed idx, free sample idx, node sample idx]; samples not in the
+// domain contribute 0 but still count in F (node.py:291-333 pads with
+// off-domain values).  SCALAR (root) tables hold the mean over the N node
+// samples, replicated over the N columns.  int32 index math throughout
+// (plan_create bounds every table and CPD below 2^31).
+__device__ float entry_partial(const DevFactor& d, int entry, int N, int c0, int c1, int cs) {
     if (d.kind == CBN_FACTOR_SCALAR) {
         float s = 0.f;
-        for (long long j = c0; j < c1; j += cs) {
+        for (int j = c0; j < c1; j += cs) {
             const int ni = d.node_sample_idx[j];
             s += ni >= 0 ? d.cpd[ni] : 0.f;
         }
         return s;
     }
-    const long long row = entry / N;
-    const int j = (int)(entry - row * N);
+    const int row = entry / N;
+    const int j = entry - row * N;
     const int ni = d.node_sample_idx[j];
     if (ni < 0) return 0.f;
-    // observed-parent part of the CPD offset (last observed parent fastest)
-    long long base = ni;
-    long long r = row;
+    int base = ni;  // observed-parent part of the CPD offset (last observed parent fastest)
+    int r = row;
     for (int p = d.n_parents - 1; p >= 0; --p) {
         if (d.ev_slot[p] >= 0) {
             const int card = d.parent_card[p];
-            const long long idx = r % card;
-            r /= card;
-            base += idx * d.cpd_stride[p];
+            const int q = r / card;
+            base += (r - q * card) * d.cpd_stride[p];
+            r = q;
         }
     }
     float s = 0.f;
-    for (long long c = c0; c < c1; c += cs) {
-        long long off = base;
-        long long cc = c;
+    for (int c = c0; c < c1; c += cs) {
+        int off = base;
+        int cc = c;
         bool ok = true;
         for (int p = d.n_parents - 1; p >= 0; --p) {
             if (d.ev_slot[p] < 0) {
-                const int smp = (int)(cc % N);
-                cc /= N;
-                const int pi = d.parent_sample_idx[p * N + smp];
+                const int q = cc / N;
+                const int pi = d.parent_sample_idx[p * N + (cc - q * N)];
+                cc = q;
                 ok &= pi >= 0;
-                off += (long long)(pi < 0 ? 0 : pi) * d.cpd_stride[p];
+                off += (pi < 0 ? 0 : pi) * d.cpd_stride[p];
             }
         }
         s += ok ? d.cpd[off] : 0.f;
@@ -198,116 +195,220 @@ __device__ float entry_partial(const DevFactor& d, long long entry, int N, long 
     return s;
 }
 
+struct BuildItem {
+    int factor;
+    int unit_begin;
+};
+
 __global__ void __launch_bounds__(kBuildThreads)
-k_build_tables(const DevFactor* __restrict__ fac, int nf, long long total_units, int N,
-               float* __restrict__ image, unsigned* __restrict__ max_bits) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && max_bits) *max_bits = 0u;
+k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ items, int n_items,
+               int total_units, int N, float* __restrict__ image) {
     const int lane = threadIdx.x & (kWave - 1);
-    const long long wave = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / kWave;
-    const long long n_waves = (long long)gridDim.x * blockDim.x / kWave;
-    for (long long u = wave; u < total_units; u += n_waves) {
-        int lo = 0, hi = nf - 1;  // factor owning unit u (wave-uniform)
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int n_waves = gridDim.x * blockDim.x / kWave;
+    for (int u = wave; u < total_units; u += n_waves) {
+        int lo = 0, hi = n_items - 1;  // build item owning unit u (wave-uniform)
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (fac[mid].unit_begin <= u) lo = mid; else hi = mid - 1;
+            if (items[mid].unit_begin <= u) lo = mid; else hi = mid - 1;
         }
-        const DevFactor& d = fac[lo];
-        const long long lu = u - d.unit_begin;
-        const long long F = d.kind == CBN_FACTOR_SCALAR ? (long long)N : d.free_combos;
+        const DevFactor& d = fac[items[lo].factor];
+        const int lu = u - items[lo].unit_begin;
+        const int F = d.kind == CBN_FACTOR_SCALAR ? N : (int)d.free_combos;
+        float* tab = image + d.table_off;
         if (d.wave_mode) {
             const float s = wave_sum(entry_partial(d, lu, N, lane, F, kWave));
-            if (lane == 0) image[d.table_off + lu] = s / (float)F;
+            if (lane == 0) tab[lu] = s / (float)F;
         } else {
-            const long long e = lu * kWave + lane;
-            if (e < d.n_entries) image[d.table_off + e] = entry_partial(d, e, N, 0, F, 1) / (float)F;
+            const int e = lu * kWave + lane;
+            if (e < d.n_entries) tab[e] = entry_partial(d, e, N, 0, F, 1) / (float)F;
         }
     }
 }
 
 // ---------------------------------------------------------------- query ----
+// Per-factor record staged in LDS for the query prologue.
+constexpr int kFqInts = 4 + 2 * kMaxP;  // img_off, kind, n_obs, pad, obs_slot[], obs_card[]
+
+struct QSlot {
+    int dom_off;
+    int card;
+};
+
+// One launch = one pass over the queries.  A block owns QB = 1024/L queries per
+// iteration; L lanes x VEC values cover one query row.
+//   fill  : LDS image <- factor tables (CPD rows copied or gathered directly;
+//           pre-built tables copied), observed-column domains, factor records
+//   A1    : sidx[q][s] = domain index of evidence column s for query q
+//           (column-major sweep: consecutive lanes read consecutive queries)
+//   A2    : offs[q][f] = LDS offset of factor f's row for query q (-1: unseen value)
+//   B     : acc = prod_f table_f[offs[q][f] + lane cols], reference factor order
+// WRITE=false folds max(acc) into *max_bits; WRITE=true stores acc / max.
 template <int VEC, bool USE_LDS, bool WRITE>
 __global__ void __launch_bounds__(kQueryThreads)
-k_query(const DevFactor* __restrict__ fac, int nf, const float* __restrict__ image,
-        int image_floats, EvPtrs ev, long long Q, int N, int L,
-        unsigned* __restrict__ max_bits, float* __restrict__ out) {
+k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slots, int ns,
+        const float* __restrict__ gimage, int table_floats, int image_floats, EvPtrs ev, long long Q,
+        int N, int L, int QB, unsigned* __restrict__ sync, unsigned* __restrict__ max_bits,
+        float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
-    const float* img = image;
-    if (USE_LDS) {
-        const float4* src = reinterpret_cast<const float4*>(image);
-        for (int i = threadIdx.x; i < image_floats / 4; i += blockDim.x) smem4[i] = src[i];
-        __syncthreads();
-        img = reinterpret_cast<const float*>(smem4);
+    float* simg = reinterpret_cast<float*>(smem4);
+    const int img_floats_lds = USE_LDS ? image_floats : 0;
+    int* fq = reinterpret_cast<int*>(simg + img_floats_lds);  // nf * kFqInts
+    QSlot* sslot = reinterpret_cast<QSlot*>(fq + nf * kFqInts);  // ns
+    int* sidx = reinterpret_cast<int*>(sslot + ns);              // QB * ns
+    int* offs = sidx + QB * ns;                                   // QB * nf
+    float* wmax = reinterpret_cast<float*>(offs + QB * nf);      // 16
+    const int tid = threadIdx.x;
+    const int nthr = blockDim.x;
+
+    // ---- fill
+    for (int f = 0; f < nf; ++f) {
+        const DevFactor& d = fac[f];
+        if (tid == 0) {
+            int* r = fq + f * kFqInts;
+            r[0] = (int)d.table_off;
+            r[1] = d.kind;
+            int n_obs = 0;
+            for (int p = 0; p < d.n_parents; ++p) {
+                if (d.ev_slot[p] >= 0) {
+                    r[4 + n_obs] = d.ev_slot[p];
+                    r[4 + kMaxP + n_obs] = d.parent_card[p];
+                    ++n_obs;
+                }
+            }
+            r[2] = n_obs;
+        }
+        if (USE_LDS) {
+            float* dst = simg + d.table_off;
+            const int ne = (int)d.n_entries;
+            if (d.fill == 1) {  // all parents observed, node samples == node domain: the CPD rows
+                if ((ne & 3) == 0) {
+                    const float4* src = reinterpret_cast<const float4*>(d.cpd);
+                    for (int i = tid; i < ne / 4; i += nthr) reinterpret_cast<float4*>(dst)[i] = src[i];
+                } else {
+                    for (int i = tid; i < ne; i += nthr) dst[i] = d.cpd[i];
+                }
+            } else if (d.fill == 2) {  // all parents observed, general node samples: gather
+                for (int e = tid; e < ne; e += nthr) {
+                    const int row = e / N;
+                    const int ni = d.node_sample_idx[e - row * N];
+                    dst[e] = ni < 0 ? 0.f : d.cpd[row * d.node_card + ni];
+                }
+            } else if (d.fill == 3) {  // root: mean of the marginal over the N samples
+                for (int e = tid; e < N; e += nthr) {
+                    float s = 0.f;
+                    for (int j = 0; j < N; ++j) {
+                        const int ni = d.node_sample_idx[j];
+                        s += ni >= 0 ? d.cpd[ni] : 0.f;
+                    }
+                    dst[e] = s / (float)N;
+                }
+            } else {  // pre-built by k_build_tables
+                const float4* src = reinterpret_cast<const float4*>(gimage + d.table_off);
+                for (int i = tid; i < (ne + 3) / 4; i += nthr) reinterpret_cast<float4*>(dst)[i] = src[i];
+            }
+        }
     }
+    if (USE_LDS) {
+        const float4* src = reinterpret_cast<const float4*>(gimage + table_floats);
+        for (int i = tid; i < (image_floats - table_floats) / 4; i += nthr)
+            reinterpret_cast<float4*>(simg + table_floats)[i] = src[i];
+    }
+    for (int s = tid; s < ns; s += nthr) sslot[s] = slots[s];
+    __syncthreads();
+    const float* img = USE_LDS ? simg : gimage;
+
     float maxv = 1.f;
     if (WRITE) maxv = __uint_as_float(*max_bits);
     float lmax = 0.f;
-    const long long items = Q * L;
-    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < items;
-         g += (long long)gridDim.x * blockDim.x) {
-        const long long q = g / L;
-        const int l = (int)(g - q * L);
-        float acc[VEC];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-        for (int f = 0; f < nf; ++f) {
-            const DevFactor& d = fac[f];
-            const int kind = d.kind;
-            if (kind == CBN_FACTOR_SCALAR) {
-                const float v = img[d.table_off];
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) acc[i] = acc[i] * v;
-                continue;
-            }
-            long long base = d.table_off + (long long)l * VEC;
-            bool ok = true;
-            if (kind == CBN_FACTOR_QUERY) {
-                long long row = 0;
-                for (int p = 0; p < d.n_parents; ++p) {
-                    const int slot = d.ev_slot[p];
-                    if (slot < 0) continue;
-                    const int card = d.parent_card[p];
-                    const float x = ev.p[slot][q];
-                    const int idx = bsearch_eq(img + d.dom_off[p], card, x);
-                    ok &= idx >= 0;
-                    row = row * card + (idx < 0 ? 0 : idx);
+    const int ql = tid / L;
+    const int l = tid - ql * L;
+    for (long long base = (long long)blockIdx.x * QB; base < Q; base += (long long)gridDim.x * QB) {
+        // A1: evidence value -> domain index (coalesced along the query axis)
+        for (int t = tid; t < QB * ns; t += nthr) {
+            const int s = t / QB;
+            const int qi = t - s * QB;
+            const long long q = base + qi;
+            int idx = -1;
+            if (q < Q) idx = bsearch_eq(img + sslot[s].dom_off, sslot[s].card, ev.p[s][q]);
+            sidx[qi * ns + s] = idx;
+        }
+        __syncthreads();
+        // A2: per (query, factor) row offset into the image
+        for (int t = tid; t < QB * nf; t += nthr) {
+            const int qi = t / nf;
+            const int f = t - qi * nf;
+            const int* r = fq + f * kFqInts;
+            int off = r[0];
+            if (r[1] == CBN_FACTOR_QUERY) {
+                int row = 0;
+                bool ok = true;
+                for (int p = 0; p < r[2]; ++p) {
+                    const int i = sidx[qi * ns + r[4 + p]];
+                    ok &= i >= 0;
+                    row = row * r[4 + kMaxP + p] + (i < 0 ? 0 : i);
                 }
-                base += row * N;
+                off = ok ? off + row * N : -1;
             }
-            if constexpr (VEC == 4) {
-                const float4 t = *reinterpret_cast<const float4*>(img + base);
-                const float tv[4] = {t.x, t.y, t.z, t.w};
+            offs[t] = off;
+        }
+        __syncthreads();
+        // B: product over factors in the reference order
+        const long long q = base + ql;
+        if (ql < QB && q < Q) {
+            float acc[VEC];
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) acc[i] = acc[i] * (ok ? tv[i] : 0.f);
+            for (int i = 0; i < VEC; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+            const int* oq = offs + ql * nf;
+#pragma unroll 4
+            for (int f = 0; f < nf; ++f) {
+                const int o = oq[f];
+                if constexpr (VEC == 4) {
+                    const float4 t = o >= 0 ? *reinterpret_cast<const float4*>(img + o + l * 4)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[0] = acc[0] * t.x;
+                    acc[1] = acc[1] * t.y;
+                    acc[2] = acc[2] * t.z;
+                    acc[3] = acc[3] * t.w;
+                } else {
+                    acc[0] = acc[0] * (o >= 0 ? img[o + l] : 0.f);
+                }
+            }
+            if (WRITE) {
+                float* o = out + q * N + (long long)l * VEC;
+                if constexpr (VEC == 4) {
+                    *reinterpret_cast<float4*>(o) =
+                        make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
+                } else {
+                    o[0] = acc[0] / maxv;
+                }
             } else {
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) acc[i] = acc[i] * (ok ? img[base + i] : 0.f);
+                for (int i = 0; i < VEC; ++i) lmax = fmaxf(lmax, acc[i]);
             }
         }
-        if (WRITE) {
-            float* o = out + q * N + (long long)l * VEC;
-            if constexpr (VEC == 4) {
-                *reinterpret_cast<float4*>(o) =
-                    make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
-            } else {
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) o[i] = acc[i] / maxv;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) lmax = fmaxf(lmax, acc[i]);
-        }
+        __syncthreads();
     }
     if (!WRITE) {
-        // per-wave maxima live after the (16-B padded) image in the dynamic LDS
-        float* wmax = reinterpret_cast<float*>(smem4) + (USE_LDS ? image_floats : 0);
         lmax = wave_max(lmax);
-        const int w = threadIdx.x / kWave;
-        if ((threadIdx.x & (kWave - 1)) == 0) wmax[w] = lmax;
+        const int w = tid / kWave;
+        if ((tid & (kWave - 1)) == 0) wmax[w] = lmax;
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             float m = 0.f;
-            for (int i = 0; i < (int)(blockDim.x / kWave); ++i) m = fmaxf(m, wmax[i]);
-            atomicMax(max_bits, __float_as_uint(m));  // values >= 0: uint order == float order
+            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
+            // values >= 0: uint order == float order.  The last block to arrive
+            // publishes the max and re-arms the plan's staging word + counter,
+            // so no memset launch is needed between calls.
+            atomicMax(&sync[0], __float_as_uint(m));
+            __threadfence();
+            const unsigned prev = atomicAdd(&sync[1], 1u);
+            if (prev == gridDim.x - 1) {
+                __threadfence();
+                const unsigned v = atomicExch(&sync[0], 0u);
+                atomicExch(&sync[1], 0u);
+                atomicExch(max_bits, v);
+            }
         }
     }
 }
@@ -329,55 +430,61 @@ int num_cu() {
 
 struct cbn_plan {
     int nf = 0;
+    int ns = 0;
     int N = 0;
-    DevFactor* d_fac = nullptr;
-    float* d_image = nullptr;     // [tables | observed-parent domains], float4 padded
-    int image_floats = 0;
-    long long table_floats = 0;
-    long long total_units = 0;
-    bool use_lds = false;
     int vec = 1;
+    int L = 1;
+    int QB = 1;
+    DevFactor* d_fac = nullptr;
+    QSlot* d_slots = nullptr;
+    BuildItem* d_build = nullptr;
+    int n_build = 0;
+    int build_units = 0;
+    float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
+    unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
+    int image_floats = 0;
+    int table_floats = 0;
+    bool use_lds = false;
+    size_t lds_bytes = 0;
     int blocks_per_cu = 1;
-    std::vector<DevFactor> h_fac;
 };
 
 namespace {
 
 template <int VEC, bool LDS, bool WRITE>
-int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out,
-                 hipStream_t s) {
-    const int L = p->N / VEC;
-    const long long items = Q * (long long)L;
-    if (items == 0) return CBN_OK;
-    long long blocks = (items + kQueryThreads - 1) / kQueryThreads;
+int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    if (Q == 0) return CBN_OK;
+    long long blocks = (Q + p->QB - 1) / p->QB;
     const long long cap = (long long)num_cu() * p->blocks_per_cu;
     if (blocks > cap) blocks = cap;
-    const size_t lds = (LDS ? (size_t)p->image_floats * sizeof(float) : 0) + kReduceLds;
-    hipLaunchKernelGGL((k_query<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads), lds, s,
-                       p->d_fac, p->nf, p->d_image, p->image_floats, ev, Q, p->N, L, max_bits, out);
+    hipLaunchKernelGGL((k_query<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads), p->lds_bytes, s,
+                       p->d_fac, p->nf, p->d_slots, p->ns, p->d_image, p->table_floats, p->image_floats, ev, Q,
+                       p->N, p->L, p->QB, p->d_sync, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
 
 template <bool WRITE>
-int dispatch_query(cbn_plan* p, long long Q, const float* const* evidence, int n_ev,
-                   unsigned* max_bits, float* out, hipStream_t s) {
-    if (n_ev < 0 || n_ev > CBN_MAX_EVIDENCE) return set_err(CBN_E_LIMIT, "n_evidence %d out of range", n_ev);
+int dispatch_query(cbn_plan* p, long long Q, const float* const* evidence, int n_ev, unsigned* max_bits,
+                   float* out, hipStream_t s) {
+    if (n_ev != p->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", p->ns, n_ev);
     EvPtrs ev;
     memset(&ev, 0, sizeof(ev));
-    for (int i = 0; i < n_ev; ++i) ev.p[i] = evidence[i];
-    if (p->vec == 4) {
+    for (int i = 0; i < n_ev; ++i) {
+        if (!evidence[i] && Q > 0) return set_err(CBN_E_ARG, "null evidence column %d", i);
+        ev.p[i] = evidence[i];
+    }
+    if (p->vec == 4)
         return p->use_lds ? launch_query<4, true, WRITE>(p, Q, ev, max_bits, out, s)
                           : launch_query<4, false, WRITE>(p, Q, ev, max_bits, out, s);
-    }
     return p->use_lds ? launch_query<1, true, WRITE>(p, Q, ev, max_bits, out, s)
                       : launch_query<1, false, WRITE>(p, Q, ev, max_bits, out, s);
 }
 
-template <int VEC, bool WRITE>
-void allow_big_lds() {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query<VEC, true, WRITE>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+template <int VEC, bool LDS, bool WRITE>
+void allow_lds(size_t bytes) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query<VEC, LDS, WRITE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 }  // namespace
@@ -440,8 +547,14 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         return set_err(CBN_E_ARG, "cbn_plan_create: bad arguments");
     *plan = nullptr;
     const int N = n_samples;
+    const int vec = (N % 4 == 0) ? 4 : 1;
+    const int L = N / vec;
+    if (L > kQueryThreads) return set_err(CBN_E_LIMIT, "N_max %d too large for one block row", N);
     std::vector<DevFactor> fac(n_factors);
-    long long off = 0, units = 0;
+    std::vector<const float*> slot_dom(CBN_MAX_EVIDENCE, nullptr);
+    std::vector<int> slot_card(CBN_MAX_EVIDENCE, 0);
+    int ns = 0;
+    long long off = 0;
     for (int f = 0; f < n_factors; ++f) {
         const cbn_factor_desc& h = factors[f];
         DevFactor& d = fac[f];
@@ -460,88 +573,128 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         d.cpd = h.cpd;
         d.node_sample_idx = h.node_sample_idx;
         d.parent_sample_idx = h.parent_sample_idx;
-        long long stride = h.node_card;
-        int n_ev = 0;
-        long long rows = 1, F = 1;
+        long long stride = h.node_card, rows = 1, F = 1;
         for (int p = h.n_parents - 1; p >= 0; --p) {
             if (h.parent_card[p] <= 0) return set_err(CBN_E_ARG, "factor %d: parent %d card", f, p);
             d.parent_card[p] = h.parent_card[p];
             d.ev_slot[p] = h.parent_ev_slot[p];
             d.cpd_stride[p] = (int)stride;
             stride *= h.parent_card[p];
-            if (stride > (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: CPD too large", f);
-            if (h.parent_ev_slot[p] >= 0) {
-                if (h.parent_ev_slot[p] >= CBN_MAX_EVIDENCE || !h.parent_domain[p])
+            if (stride >= (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: CPD too large", f);
+            const int sl = h.parent_ev_slot[p];
+            if (sl >= 0) {
+                if (sl >= CBN_MAX_EVIDENCE || !h.parent_domain[p])
                     return set_err(CBN_E_ARG, "factor %d: bad evidence slot/domain", f);
-                ++n_ev;
+                if (!slot_dom[sl]) {
+                    slot_dom[sl] = h.parent_domain[p];
+                    slot_card[sl] = h.parent_card[p];
+                } else if (slot_card[sl] != h.parent_card[p]) {
+                    return set_err(CBN_E_ARG, "evidence slot %d used with different domains", sl);
+                }
+                ns = std::max(ns, sl + 1);
                 rows *= h.parent_card[p];
             } else {
                 if (!h.parent_sample_idx) return set_err(CBN_E_ARG, "factor %d: free parent without samples", f);
                 F *= N;
-                if (F > (1LL << 40)) return set_err(CBN_E_LIMIT, "factor %d: too many free combos", f);
+                if (F >= (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: too many free combos", f);
                 d.n_free++;
             }
         }
-        if ((h.kind == CBN_FACTOR_QUERY) != (n_ev > 0))
+        if ((h.kind == CBN_FACTOR_QUERY) != (rows > 1 || d.n_parents - d.n_free > 0))
             return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
-        d.rows = rows;
-        d.free_combos = F;
-        d.n_entries = h.kind == CBN_FACTOR_SCALAR ? 1 : rows * N;
+        if (rows * (long long)N >= (1LL << 30)) return set_err(CBN_E_LIMIT, "factor %d: table too large", f);
+        d.rows = (int)rows;
+        d.free_combos = (int)F;
+        d.n_entries = (int)(rows * N);
         const long long F_eff = h.kind == CBN_FACTOR_SCALAR ? N : F;
         d.wave_mode = F_eff >= kWave ? 1 : 0;
-        d.n_units = d.wave_mode ? d.n_entries : (d.n_entries + kWave - 1) / kWave;
-        d.unit_begin = units;
-        units += d.n_units;
-        d.table_off = off;
+        d.table_off = (int)off;
         off += (d.n_entries + 3) & ~3LL;
     }
+    for (int sl = 0; sl < ns; ++sl)
+        if (!slot_dom[sl]) return set_err(CBN_E_ARG, "evidence slot %d is not used by any factor", sl);
     const long long table_floats = off;
-    // observed-parent domains appended after the tables (one copy per use)
-    std::vector<std::pair<const float*, int>> doms;
-    for (int f = 0; f < n_factors; ++f) {
-        for (int p = 0; p < fac[f].n_parents; ++p) {
-            if (fac[f].ev_slot[p] >= 0) {
-                fac[f].dom_off[p] = (int)off;
-                doms.push_back({factors[f].parent_domain[p], fac[f].parent_card[p]});
-                off += (fac[f].parent_card[p] + 3) & ~3LL;
-            }
-        }
+    std::vector<QSlot> qs(ns);
+    for (int sl = 0; sl < ns; ++sl) {
+        qs[sl].dom_off = (int)off;
+        qs[sl].card = slot_card[sl];
+        off += (slot_card[sl] + 3) & ~3LL;
     }
-    if (off > (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
+    if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
+
     cbn_plan* P = new cbn_plan();
     P->nf = n_factors;
+    P->ns = ns;
     P->N = N;
+    P->vec = vec;
+    P->L = L;
+    P->QB = kQueryThreads / L;
     P->image_floats = (int)off;
-    P->table_floats = table_floats;
-    P->total_units = units;
-    P->vec = (N % 4 == 0) ? 4 : 1;
-    const long long bytes = off * (long long)sizeof(float);
-    P->use_lds = bytes + kReduceLds <= kLdsBudget;
-    // 1024-thread blocks: at most 2 per CU (32 waves); LDS may allow only 1
-    P->blocks_per_cu = P->use_lds ? (2 * (bytes + kReduceLds) <= kLdsBudget ? 2 : 1) : 2;
-    P->h_fac = fac;
-    if (hipMalloc(&P->d_fac, sizeof(DevFactor) * n_factors) != hipSuccess ||
-        hipMalloc(&P->d_image, sizeof(float) * std::max<long long>(off, 4)) != hipSuccess) {
-        cbn_plan_destroy(P);
-        return set_err(CBN_E_HIP, "cbn_plan_create: hipMalloc failed");
+    P->table_floats = (int)table_floats;
+    const size_t side = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) +
+                        (size_t)P->QB * (ns + n_factors) * 4 + (kQueryThreads / kWave) * 4 + 16;
+    const size_t img_bytes = (size_t)off * 4;
+    P->use_lds = img_bytes + side <= (size_t)kLdsBudget;
+    P->lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
+    if (P->lds_bytes > (size_t)kLdsBudget) {
+        delete P;
+        return set_err(CBN_E_LIMIT, "plan needs %zu B of LDS even without the table image", side);
     }
-    if (hipMemcpy(P->d_fac, fac.data(), sizeof(DevFactor) * n_factors, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(P->d_image, 0, sizeof(float) * std::max<long long>(off, 4)) != hipSuccess) {
-        cbn_plan_destroy(P);
-        return set_err(CBN_E_HIP, "cbn_plan_create: upload failed");
-    }
-    long long pos = table_floats;
-    for (auto& dm : doms) {
-        if (hipMemcpy(P->d_image + pos, dm.first, sizeof(float) * dm.second, hipMemcpyDeviceToDevice) != hipSuccess) {
-            cbn_plan_destroy(P);
-            return set_err(CBN_E_HIP, "cbn_plan_create: domain copy failed");
+    P->blocks_per_cu = std::max(1, std::min(2, (int)(kLdsBudget / std::max<size_t>(P->lds_bytes, 1))));
+
+    // identity node samples (N == node card, sample j -> domain j) let the LDS
+    // fill copy CPD rows instead of gathering
+    std::vector<int> nsi(N);
+    std::vector<BuildItem> build;
+    int units = 0;
+    for (int f = 0; f < n_factors; ++f) {
+        DevFactor& d = fac[f];
+        bool direct = d.kind == CBN_FACTOR_QUERY && d.n_free == 0;
+        if (d.kind == CBN_FACTOR_SCALAR) {
+            d.fill = 3;
+        } else if (direct) {
+            bool ident = d.node_card == N;
+            if (ident) {
+                if (hipMemcpy(nsi.data(), d.node_sample_idx, sizeof(int) * N, hipMemcpyDeviceToHost) != hipSuccess) {
+                    delete P;
+                    return set_err(CBN_E_HIP, "cbn_plan_create: sample index read failed");
+                }
+                for (int j = 0; j < N && ident; ++j) ident = nsi[j] == j;
+            }
+            d.fill = ident ? 1 : 2;
+        } else {
+            d.fill = 0;
         }
-        pos += (dm.second + 3) & ~3LL;
+        if (!P->use_lds || d.fill == 0) {
+            const int nu = d.wave_mode ? d.n_entries : (d.n_entries + kWave - 1) / kWave;
+            build.push_back({f, units});
+            units += nu;
+        }
     }
-    if (P->use_lds) {
-        allow_big_lds<4, false>(); allow_big_lds<4, true>();
-        allow_big_lds<1, false>(); allow_big_lds<1, true>();
+    P->n_build = (int)build.size();
+    P->build_units = units;
+    bool ok = hipMalloc(&P->d_fac, sizeof(DevFactor) * n_factors) == hipSuccess &&
+              hipMalloc(&P->d_slots, sizeof(QSlot) * std::max(ns, 1)) == hipSuccess &&
+              hipMalloc(&P->d_build, sizeof(BuildItem) * std::max<size_t>(build.size(), 1)) == hipSuccess &&
+              hipMalloc(&P->d_image, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess &&
+              hipMalloc(&P->d_sync, sizeof(unsigned) * 4) == hipSuccess;
+    ok = ok && hipMemcpy(P->d_fac, fac.data(), sizeof(DevFactor) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && (ns == 0 || hipMemcpy(P->d_slots, qs.data(), sizeof(QSlot) * ns, hipMemcpyHostToDevice) == hipSuccess);
+    ok = ok && (build.empty() ||
+                hipMemcpy(P->d_build, build.data(), sizeof(BuildItem) * build.size(), hipMemcpyHostToDevice) == hipSuccess);
+    ok = ok && hipMemset(P->d_image, 0, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess;
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * 4) == hipSuccess;
+    for (int sl = 0; ok && sl < ns; ++sl)
+        ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
+                       hipMemcpyDeviceToDevice) == hipSuccess;
+    if (!ok) {
+        cbn_plan_destroy(P);
+        return set_err(CBN_E_HIP, "cbn_plan_create: device allocation/upload failed");
     }
+    allow_lds<4, true, false>(P->lds_bytes); allow_lds<4, true, true>(P->lds_bytes);
+    allow_lds<1, true, false>(P->lds_bytes); allow_lds<1, true, true>(P->lds_bytes);
+    allow_lds<4, false, false>(P->lds_bytes); allow_lds<4, false, true>(P->lds_bytes);
+    allow_lds<1, false, false>(P->lds_bytes); allow_lds<1, false, true>(P->lds_bytes);
     *plan = P;
     return CBN_OK;
 }
@@ -549,7 +702,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
 int cbn_plan_destroy(cbn_plan* plan) {
     if (!plan) return CBN_OK;
     if (plan->d_fac) (void)hipFree(plan->d_fac);
+    if (plan->d_slots) (void)hipFree(plan->d_slots);
+    if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);
+    if (plan->d_sync) (void)hipFree(plan->d_sync);
     delete plan;
     return CBN_OK;
 }
@@ -560,15 +716,14 @@ int64_t cbn_plan_table_bytes(const cbn_plan* plan) {
 
 int cbn_plan_uses_lds(const cbn_plan* plan) { return plan && plan->use_lds ? 1 : 0; }
 
-int cbn_plan_build_tables(cbn_plan* plan, uint32_t* max_bits, void* stream) {
+int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
     if (!plan) return set_err(CBN_E_ARG, "null plan");
+    if (plan->build_units == 0) return CBN_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    long long waves = plan->total_units;
-    long long blocks = (waves * kWave + kBuildThreads - 1) / kBuildThreads;
-    if (blocks > (long long)num_cu() * 8) blocks = (long long)num_cu() * 8;
-    if (blocks < 1) blocks = 1;
+    long long blocks = ((long long)plan->build_units * kWave + kBuildThreads - 1) / kBuildThreads;
+    blocks = std::max(1LL, std::min(blocks, (long long)num_cu() * 8));
     hipLaunchKernelGGL(k_build_tables, dim3((unsigned)blocks), dim3(kBuildThreads), 0, s, plan->d_fac,
-                       plan->nf, plan->total_units, plan->N, plan->d_image, max_bits);
+                       plan->d_build, plan->n_build, plan->build_units, plan->N, plan->d_image);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -576,8 +731,12 @@ int cbn_plan_build_tables(cbn_plan* plan, uint32_t* max_bits, void* stream) {
 int cbn_plan_query_max(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
                        uint32_t* max_bits, void* stream) {
     if (!plan || !max_bits || n_queries < 0) return set_err(CBN_E_ARG, "cbn_plan_query_max: bad arguments");
-    return dispatch_query<false>(plan, n_queries, evidence, n_evidence, max_bits, nullptr,
-                                 reinterpret_cast<hipStream_t>(stream));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (n_queries == 0) {
+        HIP_TRY(hipMemsetAsync(max_bits, 0, sizeof(uint32_t), s));
+        return CBN_OK;
+    }
+    return dispatch_query<false>(plan, n_queries, evidence, n_evidence, max_bits, nullptr, s);
 }
 
 int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
@@ -590,7 +749,7 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
 
 int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
                    uint32_t* max_bits, float* out, void* stream) {
-    int rc = cbn_plan_build_tables(plan, max_bits, stream);
+    int rc = cbn_plan_build_tables(plan, stream);
     if (rc) return rc;
     rc = cbn_plan_query_max(plan, n_queries, evidence, n_evidence, max_bits, stream);
     if (rc) return rc;

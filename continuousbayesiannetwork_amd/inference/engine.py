@@ -273,7 +273,7 @@ class InferenceEngine:
         ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
         with torch.cuda.device(device):
             s = _native.stream_ptr(device)
-            _native.check(lib.cbn_plan_build_tables(plan.handle, _native.ptr(plan.max_bits), s), "build_tables")
+            _native.check(lib.cbn_plan_build_tables(plan.handle, s), "build_tables")
             _native.check(lib.cbn_plan_query_max(plan.handle, n_queries, ptrs, len(cols),
                                                  _native.ptr(plan.max_bits), s), "query_max")
         return plan.max_bits

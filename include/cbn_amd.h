@@ -92,13 +92,15 @@ int cbn_plan_destroy(cbn_plan* plan);
 int64_t cbn_plan_table_bytes(const cbn_plan* plan);
 int cbn_plan_uses_lds(const cbn_plan* plan);
 
-/* Marginalise the free parents of every factor into its table
- * (the torch.mean(pdf, dim=parent dims) of bayesian_network.py:292) and zero
- * *max_bits.  One launch for all factors. */
-int cbn_plan_build_tables(cbn_plan* plan, uint32_t* max_bits, void* stream);
+/* Marginalise the free parents of the factors whose tables cannot be filled
+ * straight from their CPD (the torch.mean(pdf, dim=parent dims) of
+ * bayesian_network.py:292).  One launch for all such factors; a no-op when
+ * every factor is a root or has all parents observed. */
+int cbn_plan_build_tables(cbn_plan* plan, void* stream);
 
-/* Pass 1: atomically fold max over (q, j) of prod_f x_f[q, j] into *max_bits
- * (float bits; all values are >= 0).  evidence[c] is the [n_queries] float32
+/* Pass 1: *max_bits = max over (q, j) of prod_f x_f[q, j] (float bits; all
+ * values are >= 0).  The word is overwritten (no zeroing needed); a plan is
+ * used by one stream at a time.  evidence[c] is the [n_queries] float32
  * column for evidence slot c (node.py:230-256 reads them as float32). */
 int cbn_plan_query_max(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
                        int32_t n_evidence, uint32_t* max_bits, void* stream);

@@ -12,12 +12,19 @@ def make_bn(cls, edges, columns, data, device, estimator="brute_force"):
     return cls(dag, df, {"estimator_name": estimator}, {"inference_obj": "exact"}, device=device)
 
 
-def chain_data(n, d, S, seed, values=None, noise=(0.6, 0.3, 0.1)):
+def chain_data(n, d, S, seed, values=None, noise=(0.6, 0.3, 0.1), stay=None):
+    """Discrete chain X0 -> ... -> X{n-1}.  Default: X_i = X_{i-1} + noise (mod d),
+    a sparse CPT.  ``stay=p``: X_i = X_{i-1} with probability p, else uniform --
+    a dense CPT whose products along the chain stay well inside fp32 range."""
     rng = np.random.default_rng(seed)
     X = np.zeros((S, n), np.int64)
     X[:, 0] = rng.integers(0, d, S)
     for i in range(1, n):
-        X[:, i] = (X[:, i - 1] + rng.choice(len(noise), S, p=list(noise))) % d
+        if stay is not None:
+            keep = rng.random(S) < stay
+            X[:, i] = np.where(keep, X[:, i - 1], rng.integers(0, d, S))
+        else:
+            X[:, i] = (X[:, i - 1] + rng.choice(len(noise), S, p=list(noise))) % d
     vals = np.arange(d, dtype=np.float32) if values is None else np.asarray(values, np.float32)
     cols = [f"X{i}" for i in range(n)]
     edges = [(f"X{i}", f"X{i+1}") for i in range(n - 1)]
