@@ -78,7 +78,6 @@ struct DevFactor {
     int n_entries;   // rows * N
     int free_combos; // N^n_free
     int wave_mode;   // build kernel: 1 = one wave per entry (many free combos)
-    int fill;        // LDS fill: 0 pre-built, 1 CPD rows, 2 CPD gather, 3 root mean
 };
 
 struct EvPtrs {
@@ -229,90 +228,83 @@ k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ 
 // ---------------------------------------------------------------- query ----
 // Per-factor record staged in LDS for the query prologue.
 constexpr int kFqInts = 4 + 2 * kMaxP;  // img_off, kind, n_obs, pad, obs_slot[], obs_card[]
+constexpr int kUnroll = 4;
 
 struct QSlot {
-    int dom_off;
+    int dom_off;  // float offset of the sorted domain in the image
     int card;
+    int dense;    // 1: domain is exactly {0, 1, ..., card-1} -> index = value
+    int pad;
 };
 
-// One launch = one pass over the queries.  A block owns QB = 1024/L queries per
-// iteration; L lanes x VEC values cover one query row.
-//   fill  : LDS image <- factor tables (CPD rows copied or gathered directly;
-//           pre-built tables copied), observed-column domains, factor records
-//   A1    : sidx[q][s] = domain index of evidence column s for query q
-//           (column-major sweep: consecutive lanes read consecutive queries)
-//   A2    : offs[q][f] = LDS offset of factor f's row for query q (-1: unseen value)
-//   B     : acc = prod_f table_f[offs[q][f] + lane cols], reference factor order
-// WRITE=false folds max(acc) into *max_bits; WRITE=true stores acc / max.
+__device__ __forceinline__ int slot_index(const float* __restrict__ img, const QSlot& sl, float x) {
+    if (sl.dense) {
+        const int i = (int)x;
+        return (x >= 0.f && x < (float)sl.card && (float)i == x) ? i : -1;
+    }
+    return bsearch_eq(img + sl.dom_off, sl.card, x);
+}
+
+// One launch = one pass over the queries.  Block b owns the contiguous query
+// range [q0, q1); L lanes x VEC values cover one query row.
+//   fill : LDS image <- table image built by k_build_tables (+ domains), one
+//          flat float4 copy with kUnroll independent loads in flight per lane
+//   A1   : sidx[q][s] = domain index of evidence column s for query q; the
+//          evidence loads of a chunk are issued back-to-back (kUnroll per lane,
+//          consecutive lanes -> consecutive queries of one column)
+//   A2   : offs[q][f] = image offset of factor f's row for query q (-1: value
+//          outside the fitted domain -> the reference's 0 factor)
+//   B    : acc = prod_f table_f[offs[q][f] + lane cols] in the reference's
+//          factor order (bayesian_network.py:271-294)
+// WRITE=false publishes max(acc) (last block to arrive); WRITE=true stores acc/max.
 template <int VEC, bool USE_LDS, bool WRITE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slots, int ns,
-        const float* __restrict__ gimage, int table_floats, int image_floats, EvPtrs ev, long long Q,
-        int N, int L, int QB, unsigned* __restrict__ sync, unsigned* __restrict__ max_bits,
-        float* __restrict__ out) {
+        const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int L, int CH,
+        unsigned* __restrict__ sync, unsigned* __restrict__ max_bits, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
-    const int img_floats_lds = USE_LDS ? image_floats : 0;
-    int* fq = reinterpret_cast<int*>(simg + img_floats_lds);  // nf * kFqInts
-    QSlot* sslot = reinterpret_cast<QSlot*>(fq + nf * kFqInts);  // ns
-    int* sidx = reinterpret_cast<int*>(sslot + ns);              // QB * ns
-    int* offs = sidx + QB * ns;                                   // QB * nf
-    float* wmax = reinterpret_cast<float*>(offs + QB * nf);      // 16
+    int* fq = reinterpret_cast<int*>(simg + (USE_LDS ? image_floats : 0));  // nf * kFqInts
+    QSlot* sslot = reinterpret_cast<QSlot*>(fq + nf * kFqInts);             // ns
+    int* sidx = reinterpret_cast<int*>(sslot + ns);                         // CH * ns
+    int* offs = sidx + CH * ns;                                              // CH * nf
+    float* wmax = reinterpret_cast<float*>(offs + CH * nf);                 // 16
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
 
     // ---- fill
-    for (int f = 0; f < nf; ++f) {
-        const DevFactor& d = fac[f];
-        if (tid == 0) {
-            int* r = fq + f * kFqInts;
-            r[0] = (int)d.table_off;
-            r[1] = d.kind;
-            int n_obs = 0;
-            for (int p = 0; p < d.n_parents; ++p) {
-                if (d.ev_slot[p] >= 0) {
-                    r[4 + n_obs] = d.ev_slot[p];
-                    r[4 + kMaxP + n_obs] = d.parent_card[p];
-                    ++n_obs;
-                }
+    if (USE_LDS) {
+        const float4* src = reinterpret_cast<const float4*>(gimage);
+        float4* dst = smem4;
+        const int n4 = image_floats / 4;
+        for (int i0 = tid; i0 < n4; i0 += nthr * kUnroll) {
+            float4 v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int i = i0 + u * nthr;
+                if (i < n4) v[u] = src[i];
             }
-            r[2] = n_obs;
-        }
-        if (USE_LDS) {
-            float* dst = simg + d.table_off;
-            const int ne = (int)d.n_entries;
-            if (d.fill == 1) {  // all parents observed, node samples == node domain: the CPD rows
-                if ((ne & 3) == 0) {
-                    const float4* src = reinterpret_cast<const float4*>(d.cpd);
-                    for (int i = tid; i < ne / 4; i += nthr) reinterpret_cast<float4*>(dst)[i] = src[i];
-                } else {
-                    for (int i = tid; i < ne; i += nthr) dst[i] = d.cpd[i];
-                }
-            } else if (d.fill == 2) {  // all parents observed, general node samples: gather
-                for (int e = tid; e < ne; e += nthr) {
-                    const int row = e / N;
-                    const int ni = d.node_sample_idx[e - row * N];
-                    dst[e] = ni < 0 ? 0.f : d.cpd[row * d.node_card + ni];
-                }
-            } else if (d.fill == 3) {  // root: mean of the marginal over the N samples
-                for (int e = tid; e < N; e += nthr) {
-                    float s = 0.f;
-                    for (int j = 0; j < N; ++j) {
-                        const int ni = d.node_sample_idx[j];
-                        s += ni >= 0 ? d.cpd[ni] : 0.f;
-                    }
-                    dst[e] = s / (float)N;
-                }
-            } else {  // pre-built by k_build_tables
-                const float4* src = reinterpret_cast<const float4*>(gimage + d.table_off);
-                for (int i = tid; i < (ne + 3) / 4; i += nthr) reinterpret_cast<float4*>(dst)[i] = src[i];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int i = i0 + u * nthr;
+                if (i < n4) dst[i] = v[u];
             }
         }
     }
-    if (USE_LDS) {
-        const float4* src = reinterpret_cast<const float4*>(gimage + table_floats);
-        for (int i = tid; i < (image_floats - table_floats) / 4; i += nthr)
-            reinterpret_cast<float4*>(simg + table_floats)[i] = src[i];
+    for (int f = tid; f < nf; f += nthr) {
+        const DevFactor& d = fac[f];
+        int* r = fq + f * kFqInts;
+        r[0] = d.table_off;
+        r[1] = d.kind;
+        int n_obs = 0;
+        for (int p = 0; p < d.n_parents; ++p) {
+            if (d.ev_slot[p] >= 0) {
+                r[4 + n_obs] = d.ev_slot[p];
+                r[4 + kMaxP + n_obs] = d.parent_card[p];
+                ++n_obs;
+            }
+        }
+        r[2] = n_obs;
     }
     for (int s = tid; s < ns; s += nthr) sslot[s] = slots[s];
     __syncthreads();
@@ -321,24 +313,37 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
     float maxv = 1.f;
     if (WRITE) maxv = __uint_as_float(*max_bits);
     float lmax = 0.f;
-    const int ql = tid / L;
-    const int l = tid - ql * L;
-    for (long long base = (long long)blockIdx.x * QB; base < Q; base += (long long)gridDim.x * QB) {
-        // A1: evidence value -> domain index (coalesced along the query axis)
-        for (int t = tid; t < QB * ns; t += nthr) {
-            const int s = t / QB;
-            const int qi = t - s * QB;
-            const long long q = base + qi;
-            int idx = -1;
-            if (q < Q) idx = bsearch_eq(img + sslot[s].dom_off, sslot[s].card, ev.p[s][q]);
-            sidx[qi * ns + s] = idx;
+    const long long per = (Q + gridDim.x - 1) / gridDim.x;
+    const long long q0 = (long long)blockIdx.x * per;
+    const long long q1 = q0 + per < Q ? q0 + per : Q;
+    for (long long base = q0; base < q1; base += CH) {
+        const int cnt = (int)(q1 - base < CH ? q1 - base : CH);
+        // A1
+        const int pairs = cnt * ns;
+        for (int t0 = tid; t0 < pairs; t0 += nthr * kUnroll) {
+            float xv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int t = t0 + u * nthr;
+                if (t < pairs) {
+                    const int s = t / cnt;
+                    xv[u] = ev.p[s][base + (t - s * cnt)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int t = t0 + u * nthr;
+                if (t < pairs) {
+                    const int s = t / cnt;
+                    sidx[(t - s * cnt) * ns + s] = slot_index(img, sslot[s], xv[u]);
+                }
+            }
         }
         __syncthreads();
-        // A2: per (query, factor) row offset into the image
-        for (int t = tid; t < QB * nf; t += nthr) {
+        // A2
+        for (int t = tid; t < cnt * nf; t += nthr) {
             const int qi = t / nf;
-            const int f = t - qi * nf;
-            const int* r = fq + f * kFqInts;
+            const int* r = fq + (t - qi * nf) * kFqInts;
             int off = r[0];
             if (r[1] == CBN_FACTOR_QUERY) {
                 int row = 0;
@@ -353,13 +358,14 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
             offs[t] = off;
         }
         __syncthreads();
-        // B: product over factors in the reference order
-        const long long q = base + ql;
-        if (ql < QB && q < Q) {
+        // B
+        for (int it = tid; it < cnt * L; it += nthr) {
+            const int qi = it / L;
+            const int l = it - qi * L;
             float acc[VEC];
 #pragma unroll
             for (int i = 0; i < VEC; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-            const int* oq = offs + ql * nf;
+            const int* oq = offs + qi * nf;
 #pragma unroll 4
             for (int f = 0; f < nf; ++f) {
                 const int o = oq[f];
@@ -375,7 +381,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
                 }
             }
             if (WRITE) {
-                float* o = out + q * N + (long long)l * VEC;
+                float* o = out + (base + qi) * N + (long long)l * VEC;
                 if constexpr (VEC == 4) {
                     *reinterpret_cast<float4*>(o) =
                         make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
@@ -434,7 +440,7 @@ struct cbn_plan {
     int N = 0;
     int vec = 1;
     int L = 1;
-    int QB = 1;
+    int CH = 1;  // queries per block chunk (LDS-sized)
     DevFactor* d_fac = nullptr;
     QSlot* d_slots = nullptr;
     BuildItem* d_build = nullptr;
@@ -454,12 +460,14 @@ namespace {
 template <int VEC, bool LDS, bool WRITE>
 int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     if (Q == 0) return CBN_OK;
-    long long blocks = (Q + p->QB - 1) / p->QB;
+    // every CU busy once there are >= 64 queries per block; a block walks its
+    // contiguous range in LDS-sized chunks of CH queries
     const long long cap = (long long)num_cu() * p->blocks_per_cu;
+    long long blocks = (Q + 63) / 64;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads), p->lds_bytes, s,
-                       p->d_fac, p->nf, p->d_slots, p->ns, p->d_image, p->table_floats, p->image_floats, ev, Q,
-                       p->N, p->L, p->QB, p->d_sync, max_bits, out);
+                       p->d_fac, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev, Q, p->N, p->L, p->CH,
+                       p->d_sync, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -615,9 +623,16 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         if (!slot_dom[sl]) return set_err(CBN_E_ARG, "evidence slot %d is not used by any factor", sl);
     const long long table_floats = off;
     std::vector<QSlot> qs(ns);
+    std::vector<float> hdom;
     for (int sl = 0; sl < ns; ++sl) {
         qs[sl].dom_off = (int)off;
         qs[sl].card = slot_card[sl];
+        hdom.resize(slot_card[sl]);
+        if (hipMemcpy(hdom.data(), slot_dom[sl], sizeof(float) * slot_card[sl], hipMemcpyDeviceToHost) != hipSuccess)
+            return set_err(CBN_E_HIP, "cbn_plan_create: domain read failed");
+        int dense = 1;
+        for (int i = 0; i < slot_card[sl] && dense; ++i) dense = hdom[i] == (float)i;
+        qs[sl].dense = dense;
         off += (slot_card[sl] + 3) & ~3LL;
     }
     if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
@@ -628,48 +643,35 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->N = N;
     P->vec = vec;
     P->L = L;
-    P->QB = kQueryThreads / L;
     P->image_floats = (int)off;
     P->table_floats = (int)table_floats;
-    const size_t side = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) +
-                        (size_t)P->QB * (ns + n_factors) * 4 + (kQueryThreads / kWave) * 4 + 16;
+    // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
+    const size_t fixed = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) + (kQueryThreads / kWave) * 4 + 64;
+    const size_t per_q = (size_t)(ns + n_factors) * 4;
     const size_t img_bytes = (size_t)off * 4;
-    P->use_lds = img_bytes + side <= (size_t)kLdsBudget;
-    P->lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
-    if (P->lds_bytes > (size_t)kLdsBudget) {
+    auto chunk_for = [&](size_t avail) -> int {
+        if (avail <= fixed) return 0;
+        size_t ch = (avail - fixed) / per_q;
+        return (int)std::min<size_t>(ch, 1024);
+    };
+    int ch = chunk_for(kLdsBudget > img_bytes ? kLdsBudget - img_bytes : 0);
+    P->use_lds = ch >= 64;
+    if (!P->use_lds) ch = chunk_for(kLdsBudget);
+    if (ch < 1) {
         delete P;
-        return set_err(CBN_E_LIMIT, "plan needs %zu B of LDS even without the table image", side);
+        return set_err(CBN_E_LIMIT, "plan needs more LDS than a CU has (nf=%d, ns=%d)", n_factors, ns);
     }
-    P->blocks_per_cu = std::max(1, std::min(2, (int)(kLdsBudget / std::max<size_t>(P->lds_bytes, 1))));
+    P->CH = ch;
+    P->lds_bytes = ((P->use_lds ? img_bytes : 0) + fixed + (size_t)ch * per_q + 15) & ~size_t(15);
+    P->blocks_per_cu = 2 * P->lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
 
-    // identity node samples (N == node card, sample j -> domain j) let the LDS
-    // fill copy CPD rows instead of gathering
-    std::vector<int> nsi(N);
     std::vector<BuildItem> build;
     int units = 0;
     for (int f = 0; f < n_factors; ++f) {
-        DevFactor& d = fac[f];
-        bool direct = d.kind == CBN_FACTOR_QUERY && d.n_free == 0;
-        if (d.kind == CBN_FACTOR_SCALAR) {
-            d.fill = 3;
-        } else if (direct) {
-            bool ident = d.node_card == N;
-            if (ident) {
-                if (hipMemcpy(nsi.data(), d.node_sample_idx, sizeof(int) * N, hipMemcpyDeviceToHost) != hipSuccess) {
-                    delete P;
-                    return set_err(CBN_E_HIP, "cbn_plan_create: sample index read failed");
-                }
-                for (int j = 0; j < N && ident; ++j) ident = nsi[j] == j;
-            }
-            d.fill = ident ? 1 : 2;
-        } else {
-            d.fill = 0;
-        }
-        if (!P->use_lds || d.fill == 0) {
-            const int nu = d.wave_mode ? d.n_entries : (d.n_entries + kWave - 1) / kWave;
-            build.push_back({f, units});
-            units += nu;
-        }
+        const DevFactor& d = fac[f];
+        const int nu = d.wave_mode ? d.n_entries : (d.n_entries + kWave - 1) / kWave;
+        build.push_back({f, units});
+        units += nu;
     }
     P->n_build = (int)build.size();
     P->build_units = units;

@@ -62,6 +62,7 @@ class Plan:
     handle: Optional[ctypes.c_void_p] = None
     keep: list = field(default_factory=list)
     max_bits: Optional[torch.Tensor] = None
+    tables_built: bool = False
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -109,8 +110,14 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
 
 
 class InferenceEngine:
-    def __init__(self, bn):
+    """``cache_tables=False`` (default) re-runs the table build on every call,
+    like the reference recomputes every factor per call; ``True`` builds each
+    plan's tables once (they depend only on the fitted CPDs and the plan) and a
+    call is then just the two query passes."""
+
+    def __init__(self, bn, cache_tables: bool = False):
         self.bn = bn
+        self.cache_tables = cache_tables
         self._plans: Dict[tuple, Plan] = {}
         self._orders: Dict[str, List[str]] = {}
         # optional (start, mid, end) torch.cuda.Event triple recorded around the
@@ -252,20 +259,38 @@ class InferenceEngine:
             raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")
         if out is None:
             out = torch.empty((n_queries, N), dtype=torch.float32, device=device)
-        if self.timing_events is not None:
-            e0, e1, e2 = self.timing_events
-            e0.record()
-            self.query_max(plan, cols, n_queries, device)
-            e1.record()
-            self.query_write(plan, cols, n_queries, plan.max_bits, out, device)
-            e2.record()
-            return out, tdom
         ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        s_ = _native.stream_ptr(device)
         with torch.cuda.device(device):
-            _native.check(lib.cbn_plan_infer(plan.handle, n_queries, ptrs, len(cols),
-                                             _native.ptr(plan.max_bits), _native.ptr(out),
-                                             _native.stream_ptr(device)), "cbn_plan_infer")
+            if self.timing_events is not None:
+                e0, e1, e2 = self.timing_events
+                e0.record()
+                self._build(plan, s_)
+                _native.check(lib.cbn_plan_query_max(plan.handle, n_queries, ptrs, len(cols),
+                                                     _native.ptr(plan.max_bits), s_), "query_max")
+                e1.record()
+                _native.check(lib.cbn_plan_query_write(plan.handle, n_queries, ptrs, len(cols),
+                                                       _native.ptr(plan.max_bits), _native.ptr(out), s_),
+                              "query_write")
+                e2.record()
+            elif self.cache_tables:
+                self._build(plan, s_)
+                _native.check(lib.cbn_plan_query_max(plan.handle, n_queries, ptrs, len(cols),
+                                                     _native.ptr(plan.max_bits), s_), "query_max")
+                _native.check(lib.cbn_plan_query_write(plan.handle, n_queries, ptrs, len(cols),
+                                                       _native.ptr(plan.max_bits), _native.ptr(out), s_),
+                              "query_write")
+            else:
+                _native.check(lib.cbn_plan_infer(plan.handle, n_queries, ptrs, len(cols),
+                                                 _native.ptr(plan.max_bits), _native.ptr(out), s_),
+                              "cbn_plan_infer")
         return out, tdom
+
+    def _build(self, plan: Plan, stream):
+        if self.cache_tables and plan.tables_built:
+            return
+        _native.check(_native.load().cbn_plan_build_tables(plan.handle, stream), "build_tables")
+        plan.tables_built = True
 
     # ---------------------------------------------- split passes (sharded) --
     def query_max(self, plan: Plan, cols: List[torch.Tensor], n_queries: int, device) -> torch.Tensor:
@@ -273,7 +298,7 @@ class InferenceEngine:
         ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
         with torch.cuda.device(device):
             s = _native.stream_ptr(device)
-            _native.check(lib.cbn_plan_build_tables(plan.handle, s), "build_tables")
+            self._build(plan, s)
             _native.check(lib.cbn_plan_query_max(plan.handle, n_queries, ptrs, len(cols),
                                                  _native.ptr(plan.max_bits), s), "query_max")
         return plan.max_bits
