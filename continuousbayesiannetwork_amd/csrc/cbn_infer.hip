@@ -111,6 +111,27 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+// Copy n4 float4 from global to LDS with LDS-DMA (global_load_lds_dwordx4: no
+// VGPR staging; one wave-instruction moves 1 KiB).  Chunk order is rotated by
+// block so the CUs do not all hit the same L2 channel at once.  Completion is
+// awaited by the caller's __syncthreads() (it waits vmcnt(0)).
+__device__ __forceinline__ void lds_dma_copy(const float* __restrict__ g, float4* lds, int n4) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int nw = blockDim.x / kWave;
+    const int nchunk = (n4 + kWave - 1) / kWave;
+    for (int c0 = wave; c0 < nchunk; c0 += nw) {
+        const int c = (c0 + (int)blockIdx.x) % nchunk;
+        const int i = c * kWave + lane;
+        if (i < n4)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + (size_t)i * 4), (lds_void_t*)(lds + c * kWave), 16,
+                                             0, 0);
+    }
+}
+
 // ---------------------------------------------------------------- fit ------
 __global__ void k_cpd_scatter(const int32_t* __restrict__ cell, const float* __restrict__ prob,
                               long long n_rows, float* __restrict__ cpd) {
@@ -269,28 +290,13 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
     int* sidx = reinterpret_cast<int*>(sslot + ns);                         // CH * ns
     int* offs = sidx + CH * ns;                                              // CH * nf
     float* wmax = reinterpret_cast<float*>(offs + CH * nf);                 // 16
+    const float** sev = reinterpret_cast<const float**>(wmax + 16);        // ns pointers
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
+    if (tid < ns) sev[tid] = ev.p[tid];
 
     // ---- fill
-    if (USE_LDS) {
-        const float4* src = reinterpret_cast<const float4*>(gimage);
-        float4* dst = smem4;
-        const int n4 = image_floats / 4;
-        for (int i0 = tid; i0 < n4; i0 += nthr * kUnroll) {
-            float4 v[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int i = i0 + u * nthr;
-                if (i < n4) v[u] = src[i];
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int i = i0 + u * nthr;
-                if (i < n4) dst[i] = v[u];
-            }
-        }
-    }
+    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);
     for (int f = tid; f < nf; f += nthr) {
         const DevFactor& d = fac[f];
         int* r = fq + f * kFqInts;
@@ -327,7 +333,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
                 const int t = t0 + u * nthr;
                 if (t < pairs) {
                     const int s = t / cnt;
-                    xv[u] = ev.p[s][base + (t - s * cnt)];
+                    xv[u] = sev[s][base + (t - s * cnt)];
                 }
             }
 #pragma unroll
@@ -419,6 +425,153 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
     }
 }
 
+// Fast path (every factor has <= kFastObs observed parents, <= kFastF factors):
+// no per-chunk barriers.  Each lane owns (query q, VEC columns); it computes
+// the row offset of every factor in registers (fully unrolled, compile-time
+// indexed), with all evidence loads of the item issued back to back; the
+// first item's loads are in flight while the block fills the LDS image.
+constexpr int kFastF = 32;
+constexpr int kFastObs = 2;
+
+struct FastF {
+    int table_off;
+    int n_obs;
+    int slot[kFastObs];
+    int card[kFastObs];
+    int pad[2];
+};
+
+template <int VEC, bool USE_LDS>
+__device__ __forceinline__ void fast_offsets(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ sslot,
+                                             const float* __restrict__ img, const float (&x)[kFastF][kFastObs],
+                                             int N, int (&off)[kFastF]) {
+#pragma unroll
+    for (int f = 0; f < kFastF; ++f) {
+        if (f < nf) {
+            const FastF& d = ff[f];
+            int o = d.table_off;
+            if (d.n_obs > 0) {
+                int row = 0;
+                bool ok = true;
+#pragma unroll
+                for (int p = 0; p < kFastObs; ++p) {
+                    if (p < d.n_obs) {
+                        const int i = slot_index(img, sslot[d.slot[p]], x[f][p]);
+                        ok &= i >= 0;
+                        row = row * d.card[p] + (i < 0 ? 0 : i);
+                    }
+                }
+                o = ok ? o + row * N : -1;
+            }
+            off[f] = o;
+        }
+    }
+}
+
+template <bool USE_LDS>
+__device__ __forceinline__ void fast_load(const FastF* __restrict__ ff, int nf, const float* const* sev, long long q,
+                                          float (&x)[kFastF][kFastObs]) {
+#pragma unroll
+    for (int f = 0; f < kFastF; ++f) {
+        if (f < nf) {
+            const FastF& d = ff[f];
+#pragma unroll
+            for (int p = 0; p < kFastObs; ++p)
+                if (p < d.n_obs) x[f][p] = sev[d.slot[p]][q];
+        }
+    }
+}
+
+template <int VEC, bool USE_LDS, bool WRITE>
+__global__ void __launch_bounds__(kQueryThreads)
+k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slots, int ns,
+             const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int L,
+             unsigned* __restrict__ sync, unsigned* __restrict__ max_bits, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float* simg = reinterpret_cast<float*>(smem4);
+    const float** sev = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // ns pointers
+    QSlot* sslot = reinterpret_cast<QSlot*>(sev + CBN_MAX_EVIDENCE);
+    float* wmax = reinterpret_cast<float*>(sslot + ns);
+    const int tid = threadIdx.x;
+    const int nthr = blockDim.x;
+    const long long per = (Q + gridDim.x - 1) / gridDim.x;
+    const long long q0 = (long long)blockIdx.x * per;
+    const long long q1 = q0 + per < Q ? q0 + per : Q;
+    const long long i_end = q1 * L;
+    long long it = q0 * L + tid;
+    if (tid < ns) sev[tid] = ev.p[tid];  // kernel-arg array -> LDS (no scratch for the dynamic index)
+    __syncthreads();
+
+    float x[kFastF][kFastObs];
+    if (it < i_end) fast_load<USE_LDS>(ff, nf, sev, it / L, x);  // in flight during the fill
+
+    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);
+    for (int s = tid; s < ns; s += nthr) sslot[s] = slots[s];
+    __syncthreads();
+    const float* img = USE_LDS ? simg : gimage;
+
+    float maxv = 1.f;
+    if (WRITE) maxv = __uint_as_float(*max_bits);
+    float lmax = 0.f;
+    for (; it < i_end; it += nthr) {
+        const long long q = it / L;
+        const int l = (int)(it - q * L);
+        int off[kFastF];
+        fast_offsets<VEC, USE_LDS>(ff, nf, sslot, img, x, N, off);
+        const long long nxt = it + nthr;
+        if (nxt < i_end) fast_load<USE_LDS>(ff, nf, sev, nxt / L, x);  // next item's loads
+        float acc[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+#pragma unroll
+        for (int f = 0; f < kFastF; ++f) {
+            if (f < nf) {
+                const int o = off[f];
+                if constexpr (VEC == 4) {
+                    const float4 t = o >= 0 ? *reinterpret_cast<const float4*>(img + o + l * 4)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[0] = acc[0] * t.x;
+                    acc[1] = acc[1] * t.y;
+                    acc[2] = acc[2] * t.z;
+                    acc[3] = acc[3] * t.w;
+                } else {
+                    acc[0] = acc[0] * (o >= 0 ? img[o + l] : 0.f);
+                }
+            }
+        }
+        if (WRITE) {
+            float* o = out + q * N + (long long)l * VEC;
+            if constexpr (VEC == 4) {
+                *reinterpret_cast<float4*>(o) = make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
+            } else {
+                o[0] = acc[0] / maxv;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) lmax = fmaxf(lmax, acc[i]);
+        }
+    }
+    if (!WRITE) {
+        lmax = wave_max(lmax);
+        const int w = tid / kWave;
+        if ((tid & (kWave - 1)) == 0) wmax[w] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
+            atomicMax(&sync[0], __float_as_uint(m));
+            __threadfence();
+            const unsigned prev = atomicAdd(&sync[1], 1u);
+            if (prev == gridDim.x - 1) {
+                __threadfence();
+                const unsigned v = atomicExch(&sync[0], 0u);
+                atomicExch(&sync[1], 0u);
+                atomicExch(max_bits, v);
+            }
+        }
+    }
+}
+
 int g_num_cu = 0;
 
 int num_cu() {
@@ -448,6 +601,9 @@ struct cbn_plan {
     int build_units = 0;
     float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
     unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
+    FastF* d_fast = nullptr;     // fast-path factor records (nullptr: generic kernel)
+    size_t fast_lds_bytes = 0;
+    int fast_blocks_per_cu = 1;
     int image_floats = 0;
     int table_floats = 0;
     bool use_lds = false;
@@ -458,8 +614,21 @@ struct cbn_plan {
 namespace {
 
 template <int VEC, bool LDS, bool WRITE>
+int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
+    long long blocks = (Q * p->L + kQueryThreads - 1) / kQueryThreads;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL((k_query_fast<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads),
+                       p->fast_lds_bytes, s, p->d_fast, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev,
+                       Q, p->N, p->L, p->d_sync, max_bits, out);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+template <int VEC, bool LDS, bool WRITE>
 int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     if (Q == 0) return CBN_OK;
+    if (p->d_fast) return launch_fast<VEC, LDS, WRITE>(p, Q, ev, max_bits, out, s);
     // every CU busy once there are >= 64 queries per block; a block walks its
     // contiguous range in LDS-sized chunks of CH queries
     const long long cap = (long long)num_cu() * p->blocks_per_cu;
@@ -492,6 +661,8 @@ int dispatch_query(cbn_plan* p, long long Q, const float* const* evidence, int n
 template <int VEC, bool LDS, bool WRITE>
 void allow_lds(size_t bytes) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query<VEC, LDS, WRITE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VEC, LDS, WRITE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
@@ -646,7 +817,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->image_floats = (int)off;
     P->table_floats = (int)table_floats;
     // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
-    const size_t fixed = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) + (kQueryThreads / kWave) * 4 + 64;
+    const size_t fixed = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) + (kQueryThreads / kWave) * 4 +
+                         (size_t)CBN_MAX_EVIDENCE * sizeof(void*) + 64;
     const size_t per_q = (size_t)(ns + n_factors) * 4;
     const size_t img_bytes = (size_t)off * 4;
     auto chunk_for = [&](size_t avail) -> int {
@@ -675,6 +847,38 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     }
     P->n_build = (int)build.size();
     P->build_units = units;
+
+    // fast path eligibility: <= kFastF factors, <= kFastObs observed parents each
+    bool fast = n_factors <= kFastF;
+    std::vector<FastF> ffv(n_factors);
+    for (int f = 0; f < n_factors && fast; ++f) {
+        FastF& r = ffv[f];
+        memset(&r, 0, sizeof(r));
+        r.table_off = fac[f].table_off;
+        for (int p = 0; p < fac[f].n_parents; ++p) {
+            if (fac[f].ev_slot[p] >= 0) {
+                if (r.n_obs == kFastObs) { fast = false; break; }
+                r.slot[r.n_obs] = fac[f].ev_slot[p];
+                r.card[r.n_obs] = fac[f].parent_card[p];
+                ++r.n_obs;
+            }
+        }
+    }
+    const size_t fast_side = (size_t)CBN_MAX_EVIDENCE * sizeof(void*) + (size_t)ns * sizeof(QSlot) +
+                             (kQueryThreads / kWave) * 4 + 64;
+    if (fast) {
+        const bool lds_ok = img_bytes + fast_side <= (size_t)kLdsBudget;
+        if (lds_ok != P->use_lds) fast = lds_ok && P->use_lds;  // keep one LDS mode per plan
+    }
+    if (fast) {
+        P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + fast_side + 15) & ~size_t(15);
+        P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
+        if (hipMalloc(&P->d_fast, sizeof(FastF) * n_factors) != hipSuccess ||
+            hipMemcpy(P->d_fast, ffv.data(), sizeof(FastF) * n_factors, hipMemcpyHostToDevice) != hipSuccess) {
+            cbn_plan_destroy(P);
+            return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
+        }
+    }
     bool ok = hipMalloc(&P->d_fac, sizeof(DevFactor) * n_factors) == hipSuccess &&
               hipMalloc(&P->d_slots, sizeof(QSlot) * std::max(ns, 1)) == hipSuccess &&
               hipMalloc(&P->d_build, sizeof(BuildItem) * std::max<size_t>(build.size(), 1)) == hipSuccess &&
@@ -693,10 +897,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         cbn_plan_destroy(P);
         return set_err(CBN_E_HIP, "cbn_plan_create: device allocation/upload failed");
     }
-    allow_lds<4, true, false>(P->lds_bytes); allow_lds<4, true, true>(P->lds_bytes);
-    allow_lds<1, true, false>(P->lds_bytes); allow_lds<1, true, true>(P->lds_bytes);
-    allow_lds<4, false, false>(P->lds_bytes); allow_lds<4, false, true>(P->lds_bytes);
-    allow_lds<1, false, false>(P->lds_bytes); allow_lds<1, false, true>(P->lds_bytes);
+    allow_lds<4, true, false>(kLdsBudget); allow_lds<4, true, true>(kLdsBudget);
+    allow_lds<1, true, false>(kLdsBudget); allow_lds<1, true, true>(kLdsBudget);
+    allow_lds<4, false, false>(kLdsBudget); allow_lds<4, false, true>(kLdsBudget);
+    allow_lds<1, false, false>(kLdsBudget); allow_lds<1, false, true>(kLdsBudget);
     *plan = P;
     return CBN_OK;
 }
@@ -708,6 +912,7 @@ int cbn_plan_destroy(cbn_plan* plan) {
     if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);
     if (plan->d_sync) (void)hipFree(plan->d_sync);
+    if (plan->d_fast) (void)hipFree(plan->d_fast);
     delete plan;
     return CBN_OK;
 }

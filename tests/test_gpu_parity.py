@@ -203,3 +203,53 @@ def test_domain_index(gpu):
     dom = torch.tensor([-1.5, 0.25, 2.0, 7.0], device=gpu)
     v = torch.tensor([0.25, 7.0, 3.0, -1.5, 8.0, -9.0], device=gpu)
     assert domain_index(v, dom).cpu().tolist() == [1, 3, -1, 0, -1, -1]
+
+
+def _star_data(k, d, S, seed):
+    """k root parents -> one child (C depends on all parents)."""
+    rng = np.random.default_rng(seed)
+    P = rng.integers(0, d, (S, k))
+    C = (P.sum(1) + rng.integers(0, 3, S)) % d
+    X = np.concatenate([P, C[:, None]], 1).astype(np.float32)
+    cols = [f"P{i}" for i in range(k)] + ["C"]
+    return X, cols, [(f"P{i}", "C") for i in range(k)]
+
+
+@pytest.mark.parametrize("k,d,N", [(3, 16, 16), (4, 6, 6), (3, 5, 4)])
+def test_many_observed_parents_generic_and_global_paths(k, d, N, gpu):
+    """> 2 observed parents (generic kernel); k=3, d=16 makes a 256 KiB table
+    image, beyond one CU's LDS (global-memory variant)."""
+    data, cols, edges = _star_data(k, d, 40000, k * 10 + d)
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = sample_evidence(data, cols, [f"P{i}" for i in range(k)], 700, 3, missing_frac=0.05)
+    random.seed(1)
+    ref, rdom = ora.infer("C", ev, N)
+    random.seed(1)
+    pdf, dom = bn.infer("C", _t(ev, gpu), N_max=N)
+    np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
+    np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
+def test_more_factors_than_fast_path(gpu):
+    """40 ancestors (> 32 fast-path factors) and partial evidence (SHARED + QUERY mix)."""
+    data, cols, edges = chain_data(40, 3, 4000, 21, stay=0.7)
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = sample_evidence(data, cols, ["X38", "X20", "X3"], 900, 4)
+    ref, rdom = ora.infer("X39", ev, 3)
+    pdf, dom = bn.infer("X39", _t(ev, gpu), N_max=3)
+    np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
+def test_table_cache_mode_matches(gpu):
+    data, cols, edges = chain_data(12, 8, 20000, 5, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = _t(sample_evidence(data, cols, [c for c in cols if c != "X11"], 4097, 6), gpu)
+    a, _ = bn.infer("X11", ev, N_max=8)
+    a = a.clone()
+    bn.engine.cache_tables = True
+    b, _ = bn.infer("X11", ev, N_max=8)
+    c, _ = bn.infer("X11", ev, N_max=8)
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    np.testing.assert_array_equal(a.cpu().numpy(), c.cpu().numpy())
