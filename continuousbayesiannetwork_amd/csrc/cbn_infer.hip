@@ -27,6 +27,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -111,7 +112,40 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Diagnostic build only (-DCBN_STAMPS): per-wave s_memtime stamps of the query
+// kernels' phases into a debug buffer (never read by the kernels themselves).
+#ifdef CBN_STAMPS
+__device__ unsigned long long* g_stamps = nullptr;
+#define CBN_STAMP(k)                                                                          \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long _t = __builtin_amdgcn_s_memtime();                                 \
+        if (g_stamps && (threadIdx.x & 63) == 0)                                              \
+            g_stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 8 + (k)] = _t; \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+#else
+#define CBN_STAMP(k) do {} while (0)
+#endif
+
+// Diagnostic build only (-DCBN_CHECKED): validate global addresses in the
+// fast query kernel before use; a violation is recorded and the access skipped.
+#ifdef CBN_CHECKED
+__device__ unsigned* g_dbg = nullptr;
+#define CBN_OK_OR(cond, code) ((cond) ? true : (g_dbg ? (atomicOr(g_dbg, 1u << (code)), atomicAdd(g_dbg + 1 + (code), 1u), false) : false))
+#else
+#define CBN_OK_OR(cond, code) true
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) float gfloat_t;
+
+// Load through a pointer that came from LDS as a GLOBAL load: a generic
+// pointer compiles to flat_load, which the compiler fences with vmcnt(0) +
+// lgkmcnt(0) and so serialises a batch of evidence loads.
+__device__ __forceinline__ float gload(const float* p, long long i) {
+    return ((gfloat_t*)p)[i];
+}
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
 // Copy n4 float4 from global to LDS with LDS-DMA (global_load_lds_dwordx4: no
@@ -126,7 +160,7 @@ __device__ __forceinline__ void lds_dma_copy(const float* __restrict__ g, float4
     for (int c0 = wave; c0 < nchunk; c0 += nw) {
         const int c = (c0 + (int)blockIdx.x) % nchunk;
         const int i = c * kWave + lane;
-        if (i < n4)
+        if (i < n4 && CBN_OK_OR(i >= 0, 0))
             __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + (size_t)i * 4), (lds_void_t*)(lds + c * kWave), 16,
                                              0, 0);
     }
@@ -333,7 +367,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
                 const int t = t0 + u * nthr;
                 if (t < pairs) {
                     const int s = t / cnt;
-                    xv[u] = sev[s][base + (t - s * cnt)];
+                    xv[u] = gload(sev[s], base + (t - s * cnt));
                 }
             }
 #pragma unroll
@@ -425,13 +459,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
     }
 }
 
-// Fast path (every factor has <= kFastObs observed parents, <= kFastF factors):
-// no per-chunk barriers.  Each lane owns (query q, VEC columns); it computes
-// the row offset of every factor in registers (fully unrolled, compile-time
-// indexed), with all evidence loads of the item issued back to back; the
-// first item's loads are in flight while the block fills the LDS image.
-constexpr int kFastF = 32;
-constexpr int kFastObs = 2;
+constexpr int kFastObs = 2;  // fast path: observed parents per factor
 
 struct FastF {
     int table_off;
@@ -441,120 +469,183 @@ struct FastF {
     int pad[2];
 };
 
-template <int VEC, bool USE_LDS>
-__device__ __forceinline__ void fast_offsets(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ sslot,
-                                             const float* __restrict__ img, const float (&x)[kFastF][kFastObs],
-                                             int N, int (&off)[kFastF]) {
-#pragma unroll
-    for (int f = 0; f < kFastF; ++f) {
-        if (f < nf) {
-            const FastF& d = ff[f];
-            int o = d.table_off;
-            if (d.n_obs > 0) {
-                int row = 0;
-                bool ok = true;
-#pragma unroll
-                for (int p = 0; p < kFastObs; ++p) {
-                    if (p < d.n_obs) {
-                        const int i = slot_index(img, sslot[d.slot[p]], x[f][p]);
-                        ok &= i >= 0;
-                        row = row * d.card[p] + (i < 0 ? 0 : i);
-                    }
-                }
-                o = ok ? o + row * N : -1;
-            }
-            off[f] = o;
-        }
-    }
-}
+// Per-factor record, built once per block in LDS from FastF + the evidence
+// column pointers: one item reads each record with independent ds_read_b128s
+// (no scalar-load -> LDS -> global dependency chain per factor).
+struct alignas(16) FastRec {
+    int table_off;
+    int n_obs;
+    int card[kFastObs];   // bit 30: domain is {0..card-1} (index = value)
+    int dom_off[kFastObs];
+    const float* col[kFastObs];
+};
+constexpr int kDenseBit = 1 << 30;
 
-template <bool USE_LDS>
-__device__ __forceinline__ void fast_load(const FastF* __restrict__ ff, int nf, const float* const* sev, long long q,
-                                          float (&x)[kFastF][kFastObs]) {
-#pragma unroll
-    for (int f = 0; f < kFastF; ++f) {
-        if (f < nf) {
-            const FastF& d = ff[f];
-#pragma unroll
-            for (int p = 0; p < kFastObs; ++p)
-                if (p < d.n_obs) x[f][p] = sev[d.slot[p]][q];
-        }
-    }
-}
+// Fast path: the L = N / (4 VPL) lanes of one query (a power of two dividing
+// 64, so a query never straddles waves) split its factors: lane l loads the
+// evidence of factors l, l+L, ... (all loads issued before any is used),
+// maps them to domain indices and writes the factors' row offsets into the
+// wave's private LDS slice; after a wave-local LDS fence every lane reads all
+// offsets and multiplies its 4*VPL columns of each factor row.  No block
+// barrier after the prologue; few registers (kLoc factors per lane).
+constexpr int kLoc = 8;
 
-template <int VEC, bool USE_LDS, bool WRITE>
+template <int VPL, bool USE_LDS, bool WRITE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slots, int ns,
              const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int L,
              unsigned* __restrict__ sync, unsigned* __restrict__ max_bits, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
-    const float** sev = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // ns pointers
-    QSlot* sslot = reinterpret_cast<QSlot*>(sev + CBN_MAX_EVIDENCE);
-    float* wmax = reinterpret_cast<float*>(sslot + ns);
+    FastRec* rec = reinterpret_cast<FastRec*>(simg + (USE_LDS ? image_floats : 0));  // nf records
+    int* woffs_all = reinterpret_cast<int*>(rec + nf);  // per wave: (64 / L) queries x nf offsets
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    const int qpw = kWave / L;  // queries per wave per round
+    int* woffs = woffs_all + wid * qpw * nf;
+    float* wmax = reinterpret_cast<float*>(woffs_all + (nthr / kWave) * qpw * nf);
     const long long per = (Q + gridDim.x - 1) / gridDim.x;
     const long long q0 = (long long)blockIdx.x * per;
     const long long q1 = q0 + per < Q ? q0 + per : Q;
     const long long i_end = q1 * L;
-    long long it = q0 * L + tid;
-    if (tid < ns) sev[tid] = ev.p[tid];  // kernel-arg array -> LDS (no scratch for the dynamic index)
-    __syncthreads();
-
-    float x[kFastF][kFastObs];
-    if (it < i_end) fast_load<USE_LDS>(ff, nf, sev, it / L, x);  // in flight during the fill
-
-    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);
-    for (int s = tid; s < ns; s += nthr) sslot[s] = slots[s];
-    __syncthreads();
+    CBN_STAMP(0);
+    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // lands while the records are built
+    if (tid < nf) {
+        const FastF& d = ff[tid];
+        FastRec r;
+        r.table_off = d.table_off;
+        r.n_obs = d.n_obs;
+        CBN_OK_OR(d.n_obs >= 0 && d.n_obs <= kFastObs && d.slot[0] < ns && d.slot[1] < ns, 5);
+#pragma unroll
+        for (int p = 0; p < kFastObs; ++p) {
+            if (p < d.n_obs && CBN_OK_OR(d.slot[p] >= 0 && d.slot[p] < ns, 6)) {
+                const QSlot sl = slots[d.slot[p]];
+                r.card[p] = d.card[p] | (sl.dense ? kDenseBit : 0);
+                r.dom_off[p] = sl.dom_off;
+                r.col[p] = ev.p[d.slot[p]];
+            } else {
+                r.card[p] = 1;
+                r.dom_off[p] = 0;
+                r.col[p] = nullptr;
+            }
+        }
+        rec[tid] = r;
+    }
+    CBN_STAMP(1);
+    __syncthreads();  // records + LDS image (waits vmcnt(0)) ready
+    CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
 
     float maxv = 1.f;
     if (WRITE) maxv = __uint_as_float(*max_bits);
     float lmax = 0.f;
-    for (; it < i_end; it += nthr) {
-        const long long q = it / L;
-        const int l = (int)(it - q * L);
-        int off[kFastF];
-        fast_offsets<VEC, USE_LDS>(ff, nf, sslot, img, x, N, off);
-        const long long nxt = it + nthr;
-        if (nxt < i_end) fast_load<USE_LDS>(ff, nf, sev, nxt / L, x);  // next item's loads
-        float acc[VEC];
+    const int qi = lane / L;  // query slot of this lane within the wave
+    const int l = lane - qi * L;
+    int* my = woffs + qi * nf;
+    bool first = true;
+    // wave-uniform round loop: a wave's 64 items are qpw whole queries
+    for (long long wbase = q0 * L + (long long)wid * kWave; wbase < i_end; wbase += nthr) {
+        const long long it = wbase + lane;
+        const bool valid = it < i_end;
+        const long long q = valid ? it / L : q0;
+        float x[kLoc][kFastObs];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-#pragma unroll
-        for (int f = 0; f < kFastF; ++f) {
+        for (int j = 0; j < kLoc; ++j) {
+            const int f = l + j * L;
             if (f < nf) {
-                const int o = off[f];
-                if constexpr (VEC == 4) {
-                    const float4 t = o >= 0 ? *reinterpret_cast<const float4*>(img + o + l * 4)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-                    acc[0] = acc[0] * t.x;
-                    acc[1] = acc[1] * t.y;
-                    acc[2] = acc[2] * t.z;
-                    acc[3] = acc[3] * t.w;
-                } else {
-                    acc[0] = acc[0] * (o >= 0 ? img[o + l] : 0.f);
+                const FastRec& r = rec[f];
+#pragma unroll
+                for (int p = 0; p < kFastObs; ++p) {
+                    if (p < r.n_obs) {
+#ifdef CBN_CHECKED
+                        bool known = false;
+                        for (int e = 0; e < ns; ++e) known |= r.col[p] == ev.p[e];
+                        if (CBN_OK_OR(known, 1) && CBN_OK_OR(q >= 0 && q < Q, 2)) x[j][p] = gload(r.col[p], q);
+                        else x[j][p] = -1.f;
+#else
+                        x[j][p] = gload(r.col[p], q);
+#endif
+                    }
                 }
             }
         }
-        if (WRITE) {
-            float* o = out + q * N + (long long)l * VEC;
-            if constexpr (VEC == 4) {
-                *reinterpret_cast<float4*>(o) = make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
-            } else {
-                o[0] = acc[0] / maxv;
-            }
-        } else {
+        if (first) CBN_STAMP(3);
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) lmax = fmaxf(lmax, acc[i]);
+        for (int j = 0; j < kLoc; ++j) {
+            const int f = l + j * L;
+            if (f < nf) {
+                const FastRec& r = rec[f];
+                int o = r.table_off;
+                if (r.n_obs > 0) {
+                    int row = 0;
+                    bool ok = true;
+#pragma unroll
+                    for (int p = 0; p < kFastObs; ++p) {
+                        if (p < r.n_obs) {
+                            const int card = r.card[p] & (kDenseBit - 1);
+                            const float xv = x[j][p];
+                            int i;
+                            if (r.card[p] & kDenseBit) {
+                                i = (int)xv;
+                                i = (xv >= 0.f && xv < (float)card && (float)i == xv) ? i : -1;
+                            } else {
+                                i = bsearch_eq(img + r.dom_off[p], card, xv);
+                            }
+                            ok &= i >= 0;
+                            row = row * card + (i < 0 ? 0 : i);
+                        }
+                    }
+                    o = ok ? o + row * N : -1;
+                }
+                my[f] = o;
+            }
         }
+        // the offsets of this query were written by lanes of this same wave:
+        // wait for the LDS writes, keep the compiler from reordering around it
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        if (first) CBN_STAMP(4);
+        constexpr int NV = 4 * VPL;  // outputs owned by this lane
+        float acc[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+#pragma unroll 4
+        for (int f = 0; f < nf; ++f) {
+            int o = my[f];
+            if (!CBN_OK_OR(o < 0 || o + (l + 1) * VPL * 4 <= image_floats, 4)) o = -1;
+            const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                const float4 t = o >= 0 ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc[4 * v + 0] = acc[4 * v + 0] * t.x;
+                acc[4 * v + 1] = acc[4 * v + 1] * t.y;
+                acc[4 * v + 2] = acc[4 * v + 2] * t.z;
+                acc[4 * v + 3] = acc[4 * v + 3] * t.w;
+            }
+        }
+        if (first) CBN_STAMP(5);
+        if (valid && CBN_OK_OR(q < Q && (long long)(l + 1) * VPL * 4 <= N, 3)) {
+            if (WRITE) {
+                float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
+                                       acc[4 * v + 3] / maxv);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // next round rewrites this wave's offsets
+        if (first) CBN_STAMP(6);
+        first = false;
     }
+    CBN_STAMP(7);
     if (!WRITE) {
         lmax = wave_max(lmax);
-        const int w = tid / kWave;
-        if ((tid & (kWave - 1)) == 0) wmax[w] = lmax;
+        if (lane == 0) wmax[wid] = lmax;
         __syncthreads();
         if (tid == 0) {
             float m = 0.f;
@@ -602,6 +693,7 @@ struct cbn_plan {
     float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
     unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
     FastF* d_fast = nullptr;     // fast-path factor records (nullptr: generic kernel)
+    int vpl = 1;                 // fast path: float4 chunks of one query row per lane
     size_t fast_lds_bytes = 0;
     int fast_blocks_per_cu = 1;
     int image_floats = 0;
@@ -613,16 +705,26 @@ struct cbn_plan {
 
 namespace {
 
-template <int VEC, bool LDS, bool WRITE>
-int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+template <int VPL, bool LDS, bool WRITE>
+int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    const int L = p->N / (4 * VPL);
     const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
-    long long blocks = (Q * p->L + kQueryThreads - 1) / kQueryThreads;
+    long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((k_query_fast<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads),
+    hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->d_fast, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev,
-                       Q, p->N, p->L, p->d_sync, max_bits, out);
+                       Q, p->N, L, p->d_sync, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
+}
+
+template <int VEC, bool LDS, bool WRITE>
+int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    switch (p->vpl) {
+        case 4: return launch_fast_v<4, LDS, WRITE>(p, Q, ev, max_bits, out, s);
+        case 2: return launch_fast_v<2, LDS, WRITE>(p, Q, ev, max_bits, out, s);
+        default: return launch_fast_v<1, LDS, WRITE>(p, Q, ev, max_bits, out, s);
+    }
 }
 
 template <int VEC, bool LDS, bool WRITE>
@@ -644,6 +746,8 @@ int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits,
 template <bool WRITE>
 int dispatch_query(cbn_plan* p, long long Q, const float* const* evidence, int n_ev, unsigned* max_bits,
                    float* out, hipStream_t s) {
+    if (!p->d_fac || !p->d_slots || !p->d_image || !p->d_sync)
+        return set_err(CBN_E_ARG, "plan has no device buffers");
     if (n_ev != p->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", p->ns, n_ev);
     EvPtrs ev;
     memset(&ev, 0, sizeof(ev));
@@ -662,8 +766,14 @@ template <int VEC, bool LDS, bool WRITE>
 void allow_lds(size_t bytes) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query<VEC, LDS, WRITE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VEC, LDS, WRITE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if constexpr (VEC == 4) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, WRITE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, WRITE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<4, LDS, WRITE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    }
 }
 
 }  // namespace
@@ -672,6 +782,20 @@ void allow_lds(size_t bytes) {
 extern "C" {
 
 int cbn_abi_version(void) { return CBN_AMD_ABI_VERSION; }
+
+#ifdef CBN_CHECKED
+int cbn_debug_set_check_buffer(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dev_ptr, sizeof(void*)));
+    return CBN_OK;
+}
+#endif
+
+#ifdef CBN_STAMPS
+int cbn_debug_set_stamp_buffer(void* dev_ptr) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)));
+    return CBN_OK;
+}
+#endif
 
 const char* cbn_last_error(void) { return g_err.c_str(); }
 
@@ -848,37 +972,6 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->n_build = (int)build.size();
     P->build_units = units;
 
-    // fast path eligibility: <= kFastF factors, <= kFastObs observed parents each
-    bool fast = n_factors <= kFastF;
-    std::vector<FastF> ffv(n_factors);
-    for (int f = 0; f < n_factors && fast; ++f) {
-        FastF& r = ffv[f];
-        memset(&r, 0, sizeof(r));
-        r.table_off = fac[f].table_off;
-        for (int p = 0; p < fac[f].n_parents; ++p) {
-            if (fac[f].ev_slot[p] >= 0) {
-                if (r.n_obs == kFastObs) { fast = false; break; }
-                r.slot[r.n_obs] = fac[f].ev_slot[p];
-                r.card[r.n_obs] = fac[f].parent_card[p];
-                ++r.n_obs;
-            }
-        }
-    }
-    const size_t fast_side = (size_t)CBN_MAX_EVIDENCE * sizeof(void*) + (size_t)ns * sizeof(QSlot) +
-                             (kQueryThreads / kWave) * 4 + 64;
-    if (fast) {
-        const bool lds_ok = img_bytes + fast_side <= (size_t)kLdsBudget;
-        if (lds_ok != P->use_lds) fast = lds_ok && P->use_lds;  // keep one LDS mode per plan
-    }
-    if (fast) {
-        P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + fast_side + 15) & ~size_t(15);
-        P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
-        if (hipMalloc(&P->d_fast, sizeof(FastF) * n_factors) != hipSuccess ||
-            hipMemcpy(P->d_fast, ffv.data(), sizeof(FastF) * n_factors, hipMemcpyHostToDevice) != hipSuccess) {
-            cbn_plan_destroy(P);
-            return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
-        }
-    }
     bool ok = hipMalloc(&P->d_fac, sizeof(DevFactor) * n_factors) == hipSuccess &&
               hipMalloc(&P->d_slots, sizeof(QSlot) * std::max(ns, 1)) == hipSuccess &&
               hipMalloc(&P->d_build, sizeof(BuildItem) * std::max<size_t>(build.size(), 1)) == hipSuccess &&
@@ -893,14 +986,66 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     for (int sl = 0; ok && sl < ns; ++sl)
         ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
                        hipMemcpyDeviceToDevice) == hipSuccess;
+    ok = ok && hipDeviceSynchronize() == hipSuccess;  // uploads complete before any launch uses them
     if (!ok) {
         cbn_plan_destroy(P);
         return set_err(CBN_E_HIP, "cbn_plan_create: device allocation/upload failed");
+    }
+
+    // fast path eligibility: N % 4 == 0, lanes per query L = N / (4 VPL) a power
+    // of two <= 64, <= kLoc factors per lane, <= kFastObs observed parents each
+    bool fast = vec == 4;
+    std::vector<FastF> ffv(n_factors);
+    for (int f = 0; f < n_factors && fast; ++f) {
+        FastF& r = ffv[f];
+        memset(&r, 0, sizeof(r));
+        r.table_off = fac[f].table_off;
+        for (int p = 0; p < fac[f].n_parents; ++p) {
+            if (fac[f].ev_slot[p] >= 0) {
+                if (r.n_obs == kFastObs) { fast = false; break; }
+                r.slot[r.n_obs] = fac[f].ev_slot[p];
+                r.card[r.n_obs] = fac[f].parent_card[p];
+                ++r.n_obs;
+            }
+        }
+    }
+    int vpl = 0, Lf = 0;
+    if (fast) {
+        int want = 2;  // 8 output values per lane (tuned on MI355X: chain20 d32)
+        if (const char* e = getenv("CBN_FAST_VPL")) want = atoi(e);
+        for (int c : {4, 2, 1}) {
+            if (c > want || (N / 4) % c) continue;
+            const int Lc = N / (4 * c);
+            if (Lc <= kWave && (kWave % Lc) == 0 && n_factors <= kLoc * Lc) { vpl = c; Lf = Lc; break; }
+        }
+        fast = vpl > 0;
+    }
+    if (fast) {
+        const size_t side = (size_t)n_factors * sizeof(FastRec) +
+                            (size_t)(kQueryThreads / kWave) * (kWave / Lf) * n_factors * 4 + (kQueryThreads / kWave) * 4 + 64;
+        const bool lds_ok = img_bytes + side <= (size_t)kLdsBudget;
+        if (!lds_ok && P->use_lds) fast = false;  // keep one LDS mode per plan
+        if (fast) {
+            P->vpl = vpl;
+            P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
+            P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
+            if (hipMalloc(&P->d_fast, sizeof(FastF) * n_factors) != hipSuccess ||
+                hipMemcpy(P->d_fast, ffv.data(), sizeof(FastF) * n_factors, hipMemcpyHostToDevice) != hipSuccess) {
+                cbn_plan_destroy(P);
+                return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
+            }
+        }
     }
     allow_lds<4, true, false>(kLdsBudget); allow_lds<4, true, true>(kLdsBudget);
     allow_lds<1, true, false>(kLdsBudget); allow_lds<1, true, true>(kLdsBudget);
     allow_lds<4, false, false>(kLdsBudget); allow_lds<4, false, true>(kLdsBudget);
     allow_lds<1, false, false>(kLdsBudget); allow_lds<1, false, true>(kLdsBudget);
+    // invariant: every buffer a launch dereferences exists (a plan missing one
+    // must never reach a kernel)
+    if (!P->d_fac || !P->d_slots || !P->d_build || !P->d_image || !P->d_sync || (fast && !P->d_fast)) {
+        cbn_plan_destroy(P);
+        return set_err(CBN_E_HIP, "cbn_plan_create: internal error, plan buffer missing");
+    }
     *plan = P;
     return CBN_OK;
 }
