@@ -459,7 +459,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
     }
 }
 
-constexpr int kFastObs = 2;  // fast path: observed parents per factor
+constexpr int kFastObs = 4;  // fast path: observed parents per factor
 
 struct FastF {
     int table_off;
@@ -721,7 +721,6 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits
 template <int VEC, bool LDS, bool WRITE>
 int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     switch (p->vpl) {
-        case 4: return launch_fast_v<4, LDS, WRITE>(p, Q, ev, max_bits, out, s);
         case 2: return launch_fast_v<2, LDS, WRITE>(p, Q, ev, max_bits, out, s);
         default: return launch_fast_v<1, LDS, WRITE>(p, Q, ev, max_bits, out, s);
     }
@@ -770,8 +769,6 @@ void allow_lds(size_t bytes) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, WRITE>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, WRITE>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<4, LDS, WRITE>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     }
 }
@@ -1013,7 +1010,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     if (fast) {
         int want = 2;  // 8 output values per lane (tuned on MI355X: chain20 d32)
         if (const char* e = getenv("CBN_FAST_VPL")) want = atoi(e);
-        for (int c : {4, 2, 1}) {
+        for (int c : {2, 1}) {  // VPL 4 exceeds 128 VGPRs at 1024 threads (spills)
             if (c > want || (N / 4) % c) continue;
             const int Lc = N / (4 * c);
             if (Lc <= kWave && (kWave % Lc) == 0 && n_factors <= kLoc * Lc) { vpl = c; Lf = Lc; break; }

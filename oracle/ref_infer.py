@@ -228,6 +228,13 @@ class OracleBN:
 
     def infer(self, target: str, evidence: Optional[Dict[str, np.ndarray]], N_max: int = 16):
         """bayesian_network.py:208-305.  Returns (pdf [Q, N], domain [Qt, N])."""
+        raw, dom = self.infer_raw(target, evidence, N_max)
+        out = raw / raw.max()
+        return out.astype(np.float32), dom
+
+    def infer_raw(self, target: str, evidence: Optional[Dict[str, np.ndarray]], N_max: int = 16):
+        """bayesian_network.py:208-295: the factor product before the global-max
+        division of :296 (used to check the sharded normalisation)."""
         order = self.ancestors(target) + [target]
         factors = {}
         tdom = None
@@ -251,7 +258,8 @@ class OracleBN:
                 dims = (1,)
             x = pdf.astype(np.float32).mean(axis=dims, dtype=np.float32)
             out = (out * x).astype(np.float32)
-        out = out / out.max()
+        if out.size == 0:
+            raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")
         if out.shape != tdom.shape:
             raise AssertionError("pdf and domain must have same shape.")
-        return out.astype(np.float32), np.ascontiguousarray(tdom)
+        return out, np.ascontiguousarray(tdom)

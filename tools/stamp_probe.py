@@ -28,7 +28,7 @@ st = buf.view(-1, 8).cpu().numpy()
 st = st[st[:, 0] > 0]
 t0 = st[:, 0].min()
 print("waves stamped:", len(st))
-names = ["entry", "records built, fill issued", "sync (fill landed)", "ev loads issued", "offsets", "products", "store", "loop end"]
+names = ["entry", "records built, fill issued", "sync (fill landed)", "ev loads issued", "offsets + wave exchange", "products", "store", "loop end"]
 for k in range(8):
     v = st[:, k] - t0
     print(f"{k} {names[k]:28s} median {np.median(v):9.0f}  min {v.min():9.0f}  max {v.max():9.0f}  (cycles since first wave entry)")
