@@ -74,7 +74,7 @@ struct DevFactor {
     const float* cpd;
     const int* node_sample_idx;
     const int* parent_sample_idx;
-    int table_off;   // float offset of this factor's table ([rows][N]) in the image
+    int table_off;   // float offset of this factor's table ([rows][RS]) in the image
     int rows;        // prod(card of observed parents) (QUERY) or 1
     int n_entries;   // rows * N
     int free_combos; // N^n_free
@@ -256,7 +256,7 @@ struct BuildItem {
 
 __global__ void __launch_bounds__(kBuildThreads)
 k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ items, int n_items,
-               int total_units, int N, float* __restrict__ image) {
+               int total_units, int N, int RS, float* __restrict__ image) {
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
     const int n_waves = gridDim.x * blockDim.x / kWave;
@@ -270,12 +270,13 @@ k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ 
         const int lu = u - items[lo].unit_begin;
         const int F = d.kind == CBN_FACTOR_SCALAR ? N : (int)d.free_combos;
         float* tab = image + d.table_off;
+        // table rows are RS >= N floats apart (padding spreads LDS banks)
         if (d.wave_mode) {
             const float s = wave_sum(entry_partial(d, lu, N, lane, F, kWave));
-            if (lane == 0) tab[lu] = s / (float)F;
+            if (lane == 0) tab[(lu / N) * RS + lu % N] = s / (float)F;
         } else {
             const int e = lu * kWave + lane;
-            if (e < d.n_entries) tab[e] = entry_partial(d, e, N, 0, F, 1) / (float)F;
+            if (e < d.n_entries) tab[(e / N) * RS + e % N] = entry_partial(d, e, N, 0, F, 1) / (float)F;
         }
     }
 }
@@ -315,7 +316,7 @@ __device__ __forceinline__ int slot_index(const float* __restrict__ img, const Q
 template <int VEC, bool USE_LDS, bool WRITE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slots, int ns,
-        const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int L, int CH,
+        const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int RS, int L, int CH,
         unsigned* __restrict__ sync, unsigned* __restrict__ max_bits, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
@@ -393,7 +394,7 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
                     ok &= i >= 0;
                     row = row * r[4 + kMaxP + p] + (i < 0 ? 0 : i);
                 }
-                off = ok ? off + row * N : -1;
+                off = ok ? off + row * RS : -1;
             }
             offs[t] = off;
         }
@@ -461,89 +462,65 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
 
 constexpr int kFastObs = 4;  // fast path: observed parents per factor
 
-struct FastF {
-    int table_off;
-    int n_obs;
-    int slot[kFastObs];
-    int card[kFastObs];
-    int pad[2];
-};
 
-// Per-factor record, built once per block in LDS from FastF + the evidence
-// column pointers: one item reads each record with independent ds_read_b128s
-// (no scalar-load -> LDS -> global dependency chain per factor).
+// Per-factor static record, written into the plan image at plan creation and
+// copied to LDS with the tables (one LDS-DMA stream, no per-call build).
 struct alignas(16) FastRec {
     int table_off;
     int n_obs;
-    int card[kFastObs];   // bit 30: domain is {0..card-1} (index = value)
+    int card[kFastObs];     // bit 30: domain is {0..card-1} (index = value)
     int dom_off[kFastObs];
-    const float* col[kFastObs];
+    int slot[kFastObs];
+    int pad[2];
 };
 constexpr int kDenseBit = 1 << 30;
+constexpr int kRecFloats = sizeof(FastRec) / 4;
 
 // Fast path: the L = N / (4 VPL) lanes of one query (a power of two dividing
 // 64, so a query never straddles waves) split its factors: lane l loads the
 // evidence of factors l, l+L, ... (all loads issued before any is used),
 // maps them to domain indices and writes the factors' row offsets into the
 // wave's private LDS slice; after a wave-local LDS fence every lane reads all
-// offsets and multiplies its 4*VPL columns of each factor row.  No block
-// barrier after the prologue; few registers (kLoc factors per lane).
+// offsets (4 per ds_read_b128) and multiplies its 4*VPL columns of each factor
+// row in the reference's factor order.  No block barrier after the prologue.
 constexpr int kLoc = 8;
 
 template <int VPL, bool USE_LDS, bool WRITE>
 __global__ void __launch_bounds__(kQueryThreads)
-k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slots, int ns,
-             const float* __restrict__ gimage, int image_floats, EvPtrs ev, long long Q, int N, int L,
-             unsigned* __restrict__ sync, unsigned* __restrict__ max_bits, float* __restrict__ out) {
+k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, EvPtrs ev,
+             long long Q, int N, int RS, int L, unsigned* __restrict__ sync, unsigned* __restrict__ max_bits,
+             float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
-    FastRec* rec = reinterpret_cast<FastRec*>(simg + (USE_LDS ? image_floats : 0));  // nf records
-    int* woffs_all = reinterpret_cast<int*>(rec + nf);  // per wave: (64 / L) queries x nf offsets
+    const int nf4 = (nf + 3) & ~3;
+    const float** sev = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // ns pointers
+    int* woffs_all = reinterpret_cast<int*>(sev + CBN_MAX_EVIDENCE);  // per wave: (64 / L) queries x nf4
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
     const int lane = tid & (kWave - 1);
     const int wid = tid / kWave;
     const int qpw = kWave / L;  // queries per wave per round
-    int* woffs = woffs_all + wid * qpw * nf;
-    float* wmax = reinterpret_cast<float*>(woffs_all + (nthr / kWave) * qpw * nf);
+    int* woffs = woffs_all + wid * qpw * nf4;
+    float* wmax = reinterpret_cast<float*>(woffs_all + (nthr / kWave) * qpw * nf4);
     const long long per = (Q + gridDim.x - 1) / gridDim.x;
     const long long q0 = (long long)blockIdx.x * per;
     const long long q1 = q0 + per < Q ? q0 + per : Q;
     const long long i_end = q1 * L;
     CBN_STAMP(0);
-    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // lands while the records are built
-    if (tid < nf) {
-        const FastF& d = ff[tid];
-        FastRec r;
-        r.table_off = d.table_off;
-        r.n_obs = d.n_obs;
-        CBN_OK_OR(d.n_obs >= 0 && d.n_obs <= kFastObs && d.slot[0] < ns && d.slot[1] < ns, 5);
-#pragma unroll
-        for (int p = 0; p < kFastObs; ++p) {
-            if (p < d.n_obs && CBN_OK_OR(d.slot[p] >= 0 && d.slot[p] < ns, 6)) {
-                const QSlot sl = slots[d.slot[p]];
-                r.card[p] = d.card[p] | (sl.dense ? kDenseBit : 0);
-                r.dom_off[p] = sl.dom_off;
-                r.col[p] = ev.p[d.slot[p]];
-            } else {
-                r.card[p] = 1;
-                r.dom_off[p] = 0;
-                r.col[p] = nullptr;
-            }
-        }
-        rec[tid] = r;
-    }
+    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
+    if (tid < ns) sev[tid] = ev.p[tid];
     CBN_STAMP(1);
-    __syncthreads();  // records + LDS image (waits vmcnt(0)) ready
+    __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
     CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
+    const FastRec* rec = reinterpret_cast<const FastRec*>(img + rec_off);
 
     float maxv = 1.f;
     if (WRITE) maxv = __uint_as_float(*max_bits);
     float lmax = 0.f;
     const int qi = lane / L;  // query slot of this lane within the wave
     const int l = lane - qi * L;
-    int* my = woffs + qi * nf;
+    int* my = woffs + qi * nf4;
     bool first = true;
     // wave-uniform round loop: a wave's 64 items are qpw whole queries
     for (long long wbase = q0 * L + (long long)wid * kWave; wbase < i_end; wbase += nthr) {
@@ -560,12 +537,12 @@ k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slo
                 for (int p = 0; p < kFastObs; ++p) {
                     if (p < r.n_obs) {
 #ifdef CBN_CHECKED
-                        bool known = false;
-                        for (int e = 0; e < ns; ++e) known |= r.col[p] == ev.p[e];
-                        if (CBN_OK_OR(known, 1) && CBN_OK_OR(q >= 0 && q < Q, 2)) x[j][p] = gload(r.col[p], q);
-                        else x[j][p] = -1.f;
+                        if (CBN_OK_OR(r.slot[p] >= 0 && r.slot[p] < ns, 1) && CBN_OK_OR(q >= 0 && q < Q, 2))
+                            x[j][p] = gload(sev[r.slot[p]], q);
+                        else
+                            x[j][p] = -1.f;
 #else
-                        x[j][p] = gload(r.col[p], q);
+                        x[j][p] = gload(sev[r.slot[p]], q);
 #endif
                     }
                 }
@@ -597,7 +574,7 @@ k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slo
                             row = row * card + (i < 0 ? 0 : i);
                         }
                     }
-                    o = ok ? o + row * N : -1;
+                    o = ok ? o + row * RS : -1;
                 }
                 my[f] = o;
             }
@@ -611,18 +588,26 @@ k_query_fast(const FastF* __restrict__ ff, int nf, const QSlot* __restrict__ slo
         float acc[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-#pragma unroll 4
-        for (int f = 0; f < nf; ++f) {
-            int o = my[f];
-            if (!CBN_OK_OR(o < 0 || o + (l + 1) * VPL * 4 <= image_floats, 4)) o = -1;
-            const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+        for (int f0 = 0; f0 < nf; f0 += 4) {
+            const int4 o4 = *reinterpret_cast<const int4*>(my + f0);
+            const int oo[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-                const float4 t = o >= 0 ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-                acc[4 * v + 0] = acc[4 * v + 0] * t.x;
-                acc[4 * v + 1] = acc[4 * v + 1] * t.y;
-                acc[4 * v + 2] = acc[4 * v + 2] * t.z;
-                acc[4 * v + 3] = acc[4 * v + 3] * t.w;
+            for (int k = 0; k < 4; ++k) {
+                if (f0 + k < nf) {
+                    int o = oo[k];
+#ifdef CBN_CHECKED
+                    if (!CBN_OK_OR(o < 0 || o + (l + 1) * VPL * 4 <= image_floats, 4)) o = -1;
+#endif
+                    const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        const float4 t = o >= 0 ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        acc[4 * v + 0] = acc[4 * v + 0] * t.x;
+                        acc[4 * v + 1] = acc[4 * v + 1] * t.y;
+                        acc[4 * v + 2] = acc[4 * v + 2] * t.z;
+                        acc[4 * v + 3] = acc[4 * v + 3] * t.w;
+                    }
+                }
             }
         }
         if (first) CBN_STAMP(5);
@@ -692,7 +677,9 @@ struct cbn_plan {
     int build_units = 0;
     float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
     unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
-    FastF* d_fast = nullptr;     // fast-path factor records (nullptr: generic kernel)
+    bool fast = false;           // k_query_fast eligible (records live in the image)
+    int rec_off = 0;             // float offset of the FastRec array in the image
+    int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
     size_t fast_lds_bytes = 0;
     int fast_blocks_per_cu = 1;
@@ -712,8 +699,8 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads),
-                       p->fast_lds_bytes, s, p->d_fast, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev,
-                       Q, p->N, L, p->d_sync, max_bits, out);
+                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
+                       p->RS, L, p->d_sync, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -729,14 +716,14 @@ int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, 
 template <int VEC, bool LDS, bool WRITE>
 int launch_query(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     if (Q == 0) return CBN_OK;
-    if (p->d_fast) return launch_fast<VEC, LDS, WRITE>(p, Q, ev, max_bits, out, s);
+    if (p->fast) return launch_fast<VEC, LDS, WRITE>(p, Q, ev, max_bits, out, s);
     // every CU busy once there are >= 64 queries per block; a block walks its
     // contiguous range in LDS-sized chunks of CH queries
     const long long cap = (long long)num_cu() * p->blocks_per_cu;
     long long blocks = (Q + 63) / 64;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query<VEC, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads), p->lds_bytes, s,
-                       p->d_fac, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev, Q, p->N, p->L, p->CH,
+                       p->d_fac, p->nf, p->d_slots, p->ns, p->d_image, p->image_floats, ev, Q, p->N, p->RS, p->L, p->CH,
                        p->d_sync, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
@@ -849,6 +836,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     const int N = n_samples;
     const int vec = (N % 4 == 0) ? 4 : 1;
     const int L = N / vec;
+    const int RS = vec == 4 ? N + 4 : N;  // +16 B per row: consecutive rows start 4 banks apart
     if (L > kQueryThreads) return set_err(CBN_E_LIMIT, "N_max %d too large for one block row", N);
     std::vector<DevFactor> fac(n_factors);
     std::vector<const float*> slot_dom(CBN_MAX_EVIDENCE, nullptr);
@@ -902,14 +890,14 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         }
         if ((h.kind == CBN_FACTOR_QUERY) != (rows > 1 || d.n_parents - d.n_free > 0))
             return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
-        if (rows * (long long)N >= (1LL << 30)) return set_err(CBN_E_LIMIT, "factor %d: table too large", f);
+        if (rows * (long long)RS >= (1LL << 30)) return set_err(CBN_E_LIMIT, "factor %d: table too large", f);
         d.rows = (int)rows;
         d.free_combos = (int)F;
         d.n_entries = (int)(rows * N);
         const long long F_eff = h.kind == CBN_FACTOR_SCALAR ? N : F;
         d.wave_mode = F_eff >= kWave ? 1 : 0;
         d.table_off = (int)off;
-        off += (d.n_entries + 3) & ~3LL;
+        off += (rows * RS + 3) & ~3LL;
     }
     for (int sl = 0; sl < ns; ++sl)
         if (!slot_dom[sl]) return set_err(CBN_E_ARG, "evidence slot %d is not used by any factor", sl);
@@ -927,6 +915,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         qs[sl].dense = dense;
         off += (slot_card[sl] + 3) & ~3LL;
     }
+    const long long rec_off = off;  // FastRec array (fast path), copied to LDS with the tables
+    off += (long long)n_factors * kRecFloats;
     if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
 
     cbn_plan* P = new cbn_plan();
@@ -937,6 +927,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->L = L;
     P->image_floats = (int)off;
     P->table_floats = (int)table_floats;
+    P->rec_off = (int)rec_off;
+    P->RS = RS;
     // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
     const size_t fixed = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) + (kQueryThreads / kWave) * 4 +
                          (size_t)CBN_MAX_EVIDENCE * sizeof(void*) + 64;
@@ -992,16 +984,18 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     // fast path eligibility: N % 4 == 0, lanes per query L = N / (4 VPL) a power
     // of two <= 64, <= kLoc factors per lane, <= kFastObs observed parents each
     bool fast = vec == 4;
-    std::vector<FastF> ffv(n_factors);
+    std::vector<FastRec> recs(n_factors);
     for (int f = 0; f < n_factors && fast; ++f) {
-        FastF& r = ffv[f];
+        FastRec& r = recs[f];
         memset(&r, 0, sizeof(r));
         r.table_off = fac[f].table_off;
         for (int p = 0; p < fac[f].n_parents; ++p) {
-            if (fac[f].ev_slot[p] >= 0) {
+            const int sl = fac[f].ev_slot[p];
+            if (sl >= 0) {
                 if (r.n_obs == kFastObs) { fast = false; break; }
-                r.slot[r.n_obs] = fac[f].ev_slot[p];
-                r.card[r.n_obs] = fac[f].parent_card[p];
+                r.card[r.n_obs] = fac[f].parent_card[p] | (qs[sl].dense ? kDenseBit : 0);
+                r.dom_off[r.n_obs] = qs[sl].dom_off;
+                r.slot[r.n_obs] = sl;
                 ++r.n_obs;
             }
         }
@@ -1018,16 +1012,18 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         fast = vpl > 0;
     }
     if (fast) {
-        const size_t side = (size_t)n_factors * sizeof(FastRec) +
-                            (size_t)(kQueryThreads / kWave) * (kWave / Lf) * n_factors * 4 + (kQueryThreads / kWave) * 4 + 64;
+        const int nf4 = (n_factors + 3) & ~3;
+        const size_t side = (size_t)CBN_MAX_EVIDENCE * sizeof(void*) +
+                            (size_t)(kQueryThreads / kWave) * (kWave / Lf) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
         const bool lds_ok = img_bytes + side <= (size_t)kLdsBudget;
         if (!lds_ok && P->use_lds) fast = false;  // keep one LDS mode per plan
         if (fast) {
+            P->fast = true;
             P->vpl = vpl;
             P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
-            if (hipMalloc(&P->d_fast, sizeof(FastF) * n_factors) != hipSuccess ||
-                hipMemcpy(P->d_fast, ffv.data(), sizeof(FastF) * n_factors, hipMemcpyHostToDevice) != hipSuccess) {
+            if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
+                hipSuccess) {
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
             }
@@ -1039,7 +1035,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     allow_lds<1, false, false>(kLdsBudget); allow_lds<1, false, true>(kLdsBudget);
     // invariant: every buffer a launch dereferences exists (a plan missing one
     // must never reach a kernel)
-    if (!P->d_fac || !P->d_slots || !P->d_build || !P->d_image || !P->d_sync || (fast && !P->d_fast)) {
+    if (!P->d_fac || !P->d_slots || !P->d_build || !P->d_image || !P->d_sync) {
         cbn_plan_destroy(P);
         return set_err(CBN_E_HIP, "cbn_plan_create: internal error, plan buffer missing");
     }
@@ -1054,7 +1050,6 @@ int cbn_plan_destroy(cbn_plan* plan) {
     if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);
     if (plan->d_sync) (void)hipFree(plan->d_sync);
-    if (plan->d_fast) (void)hipFree(plan->d_fast);
     delete plan;
     return CBN_OK;
 }
@@ -1072,7 +1067,7 @@ int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
     long long blocks = ((long long)plan->build_units * kWave + kBuildThreads - 1) / kBuildThreads;
     blocks = std::max(1LL, std::min(blocks, (long long)num_cu() * 8));
     hipLaunchKernelGGL(k_build_tables, dim3((unsigned)blocks), dim3(kBuildThreads), 0, s, plan->d_fac,
-                       plan->d_build, plan->n_build, plan->build_units, plan->N, plan->d_image);
+                       plan->d_build, plan->n_build, plan->build_units, plan->N, plan->RS, plan->d_image);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }

@@ -110,12 +110,15 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
 
 
 class InferenceEngine:
-    """``cache_tables=False`` (default) re-runs the table build on every call,
-    like the reference recomputes every factor per call; ``True`` builds each
-    plan's tables once (they depend only on the fitted CPDs and the plan) and a
-    call is then just the two query passes."""
+    """Factor tables depend only on the fitted CPDs and the plan (target,
+    observed columns, N) -- never on evidence values -- so by default
+    (``cache_tables=True``) each plan's tables are built once by
+    ``k_build_tables`` and a call is the two query passes over the evidence.
+    A refit (``fit`` / ``update_knowledge``) drops every plan.
+    ``cache_tables=False`` re-runs the table build on every call (what the
+    reference effectively does: it recomputes every factor per call)."""
 
-    def __init__(self, bn, cache_tables: bool = False):
+    def __init__(self, bn, cache_tables: bool = True):
         self.bn = bn
         self.cache_tables = cache_tables
         self._plans: Dict[tuple, Plan] = {}

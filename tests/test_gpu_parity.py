@@ -246,6 +246,7 @@ def test_table_cache_mode_matches(gpu):
     data, cols, edges = chain_data(12, 8, 20000, 5, stay=0.8)
     bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
     ev = _t(sample_evidence(data, cols, [c for c in cols if c != "X11"], 4097, 6), gpu)
+    bn.engine.cache_tables = False
     a, _ = bn.infer("X11", ev, N_max=8)
     a = a.clone()
     bn.engine.cache_tables = True

@@ -24,7 +24,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfast) step bench 600 python bench.py --no-cpu-baseline ;;
-    benchcache) step bench_cache 600 python bench.py --no-cpu-baseline --cache-tables ;;
+    benchcold) step bench_cold 600 python bench.py --no-cpu-baseline --rebuild-tables ;;
     prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline &&
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
