@@ -678,6 +678,9 @@ struct cbn_plan {
     float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
     unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
     bool fast = false;           // k_query_fast eligible (records live in the image)
+    static constexpr int kRing = 512;
+    hipEvent_t ev[kRing][3] = {};  // timing ring (created on first timed call)
+    int ev_n = 0;
     int rec_off = 0;             // float offset of the FastRec array in the image
     int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
@@ -1045,6 +1048,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
 
 int cbn_plan_destroy(cbn_plan* plan) {
     if (!plan) return CBN_OK;
+    for (int i = 0; i < cbn_plan::kRing; ++i)
+        for (int k = 0; k < 3; ++k)
+            if (plan->ev[i][k]) (void)hipEventDestroy(plan->ev[i][k]);
     if (plan->d_fac) (void)hipFree(plan->d_fac);
     if (plan->d_slots) (void)hipFree(plan->d_slots);
     if (plan->d_build) (void)hipFree(plan->d_build);
@@ -1089,6 +1095,50 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
         return set_err(CBN_E_ARG, "cbn_plan_query_write: bad arguments");
     return dispatch_query<true>(plan, n_queries, evidence, n_evidence, const_cast<uint32_t*>(max_bits), out,
                                 reinterpret_cast<hipStream_t>(stream));
+}
+
+int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+                 uint32_t* max_bits, float* out, int32_t flags, void* stream) {
+    if (!plan) return set_err(CBN_E_ARG, "null plan");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if (flags & CBN_RUN_BUILD_TABLES) {
+        rc = cbn_plan_build_tables(plan, stream);
+        if (rc) return rc;
+    }
+    hipEvent_t* e = nullptr;
+    if ((flags & CBN_RUN_TIMED) && plan->ev_n < cbn_plan::kRing) {
+        e = plan->ev[plan->ev_n];
+        for (int k = 0; k < 3; ++k)
+            if (!e[k]) HIP_TRY(hipEventCreate(&e[k]));
+        ++plan->ev_n;
+        HIP_TRY(hipEventRecord(e[0], s));
+    }
+    rc = cbn_plan_query_max(plan, n_queries, evidence, n_evidence, max_bits, stream);
+    if (rc) return rc;
+    if (e) HIP_TRY(hipEventRecord(e[1], s));
+    rc = cbn_plan_query_write(plan, n_queries, evidence, n_evidence, max_bits, out, stream);
+    if (rc) return rc;
+    if (e) HIP_TRY(hipEventRecord(e[2], s));
+    return CBN_OK;
+}
+
+int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms) {
+    if (!plan || !n_timed || !avg_max_ms || !avg_write_ms) return set_err(CBN_E_ARG, "cbn_plan_timing: bad arguments");
+    double a = 0, b = 0;
+    for (int i = 0; i < plan->ev_n; ++i) {
+        float t0 = 0, t1 = 0;
+        HIP_TRY(hipEventSynchronize(plan->ev[i][2]));
+        HIP_TRY(hipEventElapsedTime(&t0, plan->ev[i][0], plan->ev[i][1]));
+        HIP_TRY(hipEventElapsedTime(&t1, plan->ev[i][1], plan->ev[i][2]));
+        a += t0;
+        b += t1;
+    }
+    *n_timed = plan->ev_n;
+    *avg_max_ms = plan->ev_n ? (float)(a / plan->ev_n) : 0.f;
+    *avg_write_ms = plan->ev_n ? (float)(b / plan->ev_n) : 0.f;
+    plan->ev_n = 0;
+    return CBN_OK;
 }
 
 int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,

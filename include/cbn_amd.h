@@ -115,6 +115,18 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
 int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
                    int32_t n_evidence, uint32_t* max_bits, float* out, void* stream);
 
+/* query_max + query_write, preceded by build_tables when flags has
+ * CBN_RUN_BUILD_TABLES; CBN_RUN_TIMED records HIP events around the two
+ * passes on `stream` (up to 512 calls, read back by cbn_plan_timing). */
+#define CBN_RUN_BUILD_TABLES 1
+#define CBN_RUN_TIMED 2
+int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
+                 int32_t n_evidence, uint32_t* max_bits, float* out, int32_t flags, void* stream);
+
+/* Average device time (ms) of the max and write passes over the timed calls
+ * since the last read; waits for them; resets the ring. */
+int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms);
+
 #ifdef __cplusplus
 }
 #endif
