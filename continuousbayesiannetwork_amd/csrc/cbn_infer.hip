@@ -485,11 +485,18 @@ constexpr int kRecFloats = sizeof(FastRec) / 4;
 // row in the reference's factor order.  No block barrier after the prologue.
 constexpr int kLoc = 8;
 
-template <int VPL, bool USE_LDS, bool WRITE>
+// MODE 0: max pass, 1: write pass (two launches); 2: fused -- one launch, one
+// round per wave, products kept in registers across an agent-scope grid
+// barrier on the global max (all blocks co-resident: grid <= #CUs, 1 block/CU).
+constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2;
+constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
+
+template <int VPL, bool USE_LDS, int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, EvPtrs ev,
-             long long Q, int N, int RS, int L, unsigned* __restrict__ sync, unsigned* __restrict__ max_bits,
-             float* __restrict__ out) {
+             long long Q, int N, int RS, int L, unsigned* __restrict__ sync, int parity,
+             unsigned* __restrict__ max_bits, float* __restrict__ out) {
+    constexpr bool WRITE = MODE == kModeWrite;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
@@ -509,6 +516,11 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     CBN_STAMP(0);
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
     if (tid < ns) sev[tid] = ev.p[tid];
+    if (MODE == kModeFused && blockIdx.x == 0 && tid == 0) {
+        // re-arm the other parity's words for the next fused launch (nobody uses them now)
+        atomicExch(&sync[4 + 4 * (parity ^ 1)], 0u);
+        atomicExch(&sync[5 + 4 * (parity ^ 1)], 0u);
+    }
     CBN_STAMP(1);
     __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
     CBN_STAMP(2);
@@ -522,6 +534,9 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const int l = lane - qi * L;
     int* my = woffs + qi * nf4;
     bool first = true;
+    constexpr int NV = 4 * VPL;  // outputs owned by this lane
+    float acc[NV];
+    long long fq = -1;  // fused: the one query this lane holds (-1: none)
     // wave-uniform round loop: a wave's 64 items are qpw whole queries
     for (long long wbase = q0 * L + (long long)wid * kWave; wbase < i_end; wbase += nthr) {
         const long long it = wbase + lane;
@@ -584,8 +599,6 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
         if (first) CBN_STAMP(4);
-        constexpr int NV = 4 * VPL;  // outputs owned by this lane
-        float acc[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         for (int f0 = 0; f0 < nf; f0 += 4) {
@@ -612,6 +625,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         }
         if (first) CBN_STAMP(5);
         if (valid && CBN_OK_OR(q < Q && (long long)(l + 1) * VPL * 4 <= N, 3)) {
+            if (MODE == kModeFused) fq = q;
             if (WRITE) {
                 float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
 #pragma unroll
@@ -628,7 +642,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         first = false;
     }
     CBN_STAMP(7);
-    if (!WRITE) {
+    if (MODE == kModeMax) {
         lmax = wave_max(lmax);
         if (lane == 0) wmax[wid] = lmax;
         __syncthreads();
@@ -644,6 +658,39 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 atomicExch(&sync[1], 0u);
                 atomicExch(max_bits, v);
             }
+        }
+    }
+    if (MODE == kModeFused) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
+            unsigned* st = sync + 4 + 4 * parity;  // [max bits, arrivals]
+            atomicMax(&st[0], __float_as_uint(m));
+            __threadfence();
+            atomicAdd(&st[1], 1u);
+            unsigned spins = 0;
+            while (__hip_atomic_load(&st[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
+                    atomicOr(&sync[2], 1u);
+                    break;
+                }
+            }
+            const unsigned v = __hip_atomic_load(&st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wmax[0] = __uint_as_float(v);
+            if (blockIdx.x == 0) atomicExch(max_bits, v);
+        }
+        __syncthreads();
+        maxv = wmax[0];
+        if (fq >= 0) {
+            float4* o = reinterpret_cast<float4*>(out + fq * N) + l * VPL;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v)
+                o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
+                                   acc[4 * v + 3] / maxv);
         }
     }
 }
@@ -684,6 +731,8 @@ struct cbn_plan {
     int rec_off = 0;             // float offset of the FastRec array in the image
     int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
+    int fused_parity = 0;        // fused launches alternate sync-word pairs
+    bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;
     int fast_blocks_per_cu = 1;
     int image_floats = 0;
@@ -701,9 +750,25 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits
     const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE>), dim3((unsigned)blocks), dim3(kQueryThreads),
+    hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE ? kModeWrite : kModeMax>), dim3((unsigned)blocks),
+                       dim3(kQueryThreads), p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image,
+                       p->image_floats, ev, Q, p->N, p->RS, L, p->d_sync, 0, max_bits, out);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+// Single-launch path: one round per wave, so Q <= blocks * 16 waves * (64 / L);
+// blocks <= #CUs with one block per CU, so every block is resident at once.
+template <int VPL, bool LDS>
+int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    const int L = p->N / (4 * VPL);
+    const long long per_block = (long long)(kQueryThreads / kWave) * (kWave / L);
+    const long long blocks = (Q + per_block - 1) / per_block;
+    const int par = p->fused_parity;
+    p->fused_parity ^= 1;
+    hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeFused>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
-                       p->RS, L, p->d_sync, max_bits, out);
+                       p->RS, L, p->d_sync, par, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -756,11 +821,22 @@ void allow_lds(size_t bytes) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query<VEC, LDS, WRITE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if constexpr (VEC == 4) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, WRITE>),
+        constexpr int M = WRITE ? kModeWrite : kModeMax;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, M>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, WRITE>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, M>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, kModeFused>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeFused>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     }
+}
+
+long long fused_capacity(const cbn_plan* p) {
+    if (!p->fast || !p->use_lds || !p->fused_ok) return 0;
+    const int L = p->N / (4 * p->vpl);
+    return (long long)num_cu() * (kQueryThreads / kWave) * (kWave / L);
 }
 
 }  // namespace
@@ -968,13 +1044,13 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
               hipMalloc(&P->d_slots, sizeof(QSlot) * std::max(ns, 1)) == hipSuccess &&
               hipMalloc(&P->d_build, sizeof(BuildItem) * std::max<size_t>(build.size(), 1)) == hipSuccess &&
               hipMalloc(&P->d_image, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess &&
-              hipMalloc(&P->d_sync, sizeof(unsigned) * 4) == hipSuccess;
+              hipMalloc(&P->d_sync, sizeof(unsigned) * 16) == hipSuccess;
     ok = ok && hipMemcpy(P->d_fac, fac.data(), sizeof(DevFactor) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && (ns == 0 || hipMemcpy(P->d_slots, qs.data(), sizeof(QSlot) * ns, hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && (build.empty() ||
                 hipMemcpy(P->d_build, build.data(), sizeof(BuildItem) * build.size(), hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && hipMemset(P->d_image, 0, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess;
-    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * 4) == hipSuccess;
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * 16) == hipSuccess;
     for (int sl = 0; ok && sl < ns; ++sl)
         ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
                        hipMemcpyDeviceToDevice) == hipSuccess;
@@ -1029,6 +1105,19 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 hipSuccess) {
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
+            }
+            if (P->use_lds && !getenv("CBN_NO_FUSED")) {
+                // the grid barrier needs every block resident: check one block per CU fits
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+                int nb = 0;
+                const void* fn = vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>)
+                                          : reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>);
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, P->fast_lds_bytes) ==
+                        hipSuccess && nb >= 1)
+                    P->fused_ok = true;
             }
         }
     }
@@ -1114,6 +1203,20 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         ++plan->ev_n;
         HIP_TRY(hipEventRecord(e[0], s));
     }
+    if (n_queries > 0 && !(flags & CBN_RUN_TWO_PASS) && fused_capacity(plan) >= n_queries) {
+        // one launch: both passes with the products held in registers across a grid barrier
+        if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
+        if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+        EvPtrs ev;
+        memset(&ev, 0, sizeof(ev));
+        for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
+        if (e) HIP_TRY(hipEventRecord(e[1], s));
+        rc = plan->vpl == 2 ? launch_fused_v<2, true>(plan, n_queries, ev, max_bits, out, s)
+                            : launch_fused_v<1, true>(plan, n_queries, ev, max_bits, out, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[2], s));
+        return CBN_OK;
+    }
     rc = cbn_plan_query_max(plan, n_queries, evidence, n_evidence, max_bits, stream);
     if (rc) return rc;
     if (e) HIP_TRY(hipEventRecord(e[1], s));
@@ -1122,6 +1225,16 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
     if (e) HIP_TRY(hipEventRecord(e[2], s));
     return CBN_OK;
 }
+
+int cbn_plan_status(cbn_plan* plan, int32_t* status) {
+    if (!plan || !status) return set_err(CBN_E_ARG, "cbn_plan_status: bad arguments");
+    unsigned v = 0;
+    HIP_TRY(hipMemcpy(&v, plan->d_sync + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *status = (int32_t)v;
+    return CBN_OK;
+}
+
+int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
 
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms) {
     if (!plan || !n_timed || !avg_max_ms || !avg_write_ms) return set_err(CBN_E_ARG, "cbn_plan_timing: bad arguments");

@@ -141,6 +141,9 @@ class InferenceEngine:
         # record HIP events around the two query passes inside the library
         # (bench.py's per-kernel timing; read back with timing())
         self.timed = False
+        # single-launch path (both passes, grid barrier on the max) when the
+        # batch fits one round of the resident grid; False forces two launches
+        self.fused = True
         self._fast: Dict[tuple, "_FastPath"] = {}
 
     def invalidate(self):
@@ -284,7 +287,23 @@ class InferenceEngine:
             plan.tables_built = self.cache_tables
         if self.timed:
             f |= _native.CBN_RUN_TIMED
+        if not self.fused:
+            f |= _native.CBN_RUN_TWO_PASS
         return f
+
+    def check_status(self):
+        """Raise if any fused launch's grid barrier timed out (output invalid)."""
+        lib = _native.load()
+        st = ctypes.c_int32()
+        for p in self._plans.values():
+            _native.check(lib.cbn_plan_status(p.handle, ctypes.byref(st)), "status")
+            if st.value:
+                raise _native.NativeError("a single-launch inference timed out in its grid barrier "
+                                          "(not every block was resident); rerun with engine.fused = False")
+
+    def fused_capacity(self, target: str, evidence_keys, N_max: int) -> int:
+        fp = self._fast.get((target, tuple(evidence_keys), N_max))
+        return int(_native.load().cbn_plan_fused_capacity(fp.plan.handle)) if fp else 0
 
     def _run_fast(self, fp: "_FastPath", evidence, out):
         """Hot path: no plan lookup, no context managers, no re-validation

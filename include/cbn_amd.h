@@ -120,8 +120,16 @@ int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* eviden
  * passes on `stream` (up to 512 calls, read back by cbn_plan_timing). */
 #define CBN_RUN_BUILD_TABLES 1
 #define CBN_RUN_TIMED 2
+#define CBN_RUN_TWO_PASS 4  /* force max + write launches (no single-launch grid-barrier path) */
 int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
                  int32_t n_evidence, uint32_t* max_bits, float* out, int32_t flags, void* stream);
+
+/* Largest batch the single-launch path takes (0: not available for this
+ * plan); larger batches run as two launches.  Status: nonzero when a fused
+ * launch's grid barrier timed out (a block never became resident) -- its
+ * output is then invalid; reads device memory (synchronous). */
+int64_t cbn_plan_fused_capacity(const cbn_plan* plan);
+int cbn_plan_status(cbn_plan* plan, int32_t* status);
 
 /* Average device time (ms) of the max and write passes over the timed calls
  * since the last read; waits for them; resets the ring. */

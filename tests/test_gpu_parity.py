@@ -254,3 +254,26 @@ def test_table_cache_mode_matches(gpu):
     c, _ = bn.infer("X11", ev, N_max=8)
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_array_equal(a.cpu().numpy(), c.cpu().numpy())
+
+
+@pytest.mark.parametrize("Q", [1, 100, 4096, 65536, 65537])
+def test_single_launch_matches_two_launch(Q, gpu):
+    """The fused single-launch path (grid barrier on the max) is bit-identical
+    to the two-launch path; batches above its capacity fall back to two launches."""
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    ev = _t(sample_evidence(data, cols, names, Q, 9), gpu)
+    bn.engine.fused = False
+    a, _ = bn.infer("X19", ev, N_max=32)
+    a = a.clone()
+    bn.engine.fused = True
+    b, _ = bn.infer("X19", ev, N_max=32)
+    torch.cuda.synchronize()
+    bn.engine.check_status()
+    cap = bn.engine.fused_capacity("X19", names, 32)
+    assert cap >= 65536
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    if Q <= 64:
+        ref, _ = OracleBN(edges, cols, data).infer("X19", {k: v.cpu().numpy() for k, v in ev.items()}, 32)
+        np.testing.assert_allclose(b.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
