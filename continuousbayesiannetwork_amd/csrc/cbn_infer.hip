@@ -121,7 +121,7 @@ __device__ unsigned long long* g_stamps = nullptr;
         __builtin_amdgcn_sched_barrier(0);                                                    \
         unsigned long long _t = __builtin_amdgcn_s_memtime();                                 \
         if (g_stamps && (threadIdx.x & 63) == 0)                                              \
-            g_stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 8 + (k)] = _t; \
+            g_stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12 + (k)] = _t; \
         __builtin_amdgcn_sched_barrier(0);                                                    \
     } while (0)
 #else
@@ -683,7 +683,9 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
             wmax[0] = __uint_as_float(v);
             if (blockIdx.x == 0) atomicExch(max_bits, v);
         }
+        CBN_STAMP(8);
         __syncthreads();
+        CBN_STAMP(9);
         maxv = wmax[0];
         if (fq >= 0) {
             float4* o = reinterpret_cast<float4*>(out + fq * N) + l * VPL;
@@ -692,6 +694,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
                                    acc[4 * v + 3] / maxv);
         }
+        CBN_STAMP(10);
     }
 }
 

@@ -1,6 +1,6 @@
 """Diagnostic: per-wave phase stamps of the fast query kernel (build with
 -DCBN_STAMPS into libcbn_amd_stamps.so).  Prints median cycles per phase."""
-import ctypes, os, sys, subprocess
+import ctypes, os, sys
 import numpy as np
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,25 +13,32 @@ from helpers import chain_data, make_bn, sample_evidence
 dev = torch.device("cuda:0")
 lib = nat.load()
 lib.cbn_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
-buf = torch.zeros(4096 * 16 * 8, dtype=torch.int64, device=dev)
+S = 12
+buf = torch.zeros(4096 * 16 * S, dtype=torch.int64, device=dev)
 data, cols, edges = chain_data(20, 32, 200000, 3, stay=0.8)
 bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
-ev = {k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, cols[:-1], 65536, 1000).items()}
-for _ in range(20):
-    bn.infer("X19", ev, N_max=32)
+bn.engine.fused = os.environ.get("TWO_PASS") is None
+evs = []
+for b in range(8):
+    evs.append({k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, cols[:-1], 65536, 1000 + b).items()})
+for i in range(40):
+    bn.infer("X19", evs[i % 8], N_max=32)
 torch.cuda.synchronize()
 nat.check(lib.cbn_debug_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())), "stamps")
 buf.zero_()
-bn.infer("X19", ev, N_max=32)   # stamps of the write pass overwrite the max pass's
+bn.infer("X19", evs[3], N_max=32)
 torch.cuda.synchronize()
-st = buf.view(-1, 8).cpu().numpy()
+st = buf.view(-1, S).cpu().numpy()
 st = st[st[:, 0] > 0]
-t0 = st[:, 0].min()
-print("waves stamped:", len(st))
-names = ["entry", "records built, fill issued", "sync (fill landed)", "ev loads issued", "offsets + wave exchange", "products", "store", "loop end"]
-for k in range(8):
-    v = st[:, k] - t0
-    print(f"{k} {names[k]:28s} median {np.median(v):9.0f}  min {v.min():9.0f}  max {v.max():9.0f}  (cycles since first wave entry)")
-for k in range(1, 8):
-    d = st[:, k] - st[:, k - 1]
-    print(f"  d{k} {names[k]:26s} median {np.median(d):9.0f}")
+print("waves stamped:", len(st), "fused" if bn.engine.fused else "two-pass (write pass stamps)")
+names = ["entry", "fill issued + sev", "sync (fill landed)", "ev loads issued", "offsets + wave exchange",
+         "products", "store/acc", "loop end", "barrier passed (tid0)", "block sync after barrier", "stored"]
+for k in range(1, 11):
+    ok = (st[:, k] > 0) & (st[:, k - 1] > 0)
+    if ok.sum() == 0:
+        continue
+    d = st[ok, k] - st[ok, k - 1]
+    print(f"  d{k:<2} {names[k]:28s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}  max {d.max():9.0f}")
+tot = st[:, 10] - st[:, 0] if bn.engine.fused else st[:, 7] - st[:, 0]
+tot = tot[tot > 0]
+print("  total per wave: median", np.median(tot), "max", tot.max())
