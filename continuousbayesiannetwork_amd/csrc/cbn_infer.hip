@@ -91,6 +91,17 @@ struct ColPtrs {
     int stride[kMaxP + 1];
 };
 
+// Memory-side read of a counter: a returning atomic add of 0, in asm because
+// LLVM folds an idempotent atomicAdd(p, 0) into an L2-served sc1 load -- and an
+// XCD's L2 copy of a line other XCDs keep adding to can stay stale for microseconds.
+__device__ __forceinline__ unsigned atomic_read_mem(unsigned* p) {
+    unsigned v;
+    const unsigned zero = 0u;
+    asm volatile("global_atomic_add %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
+                 : "=v"(v) : "v"(p), "v"(zero) : "memory");
+    return v;
+}
+
 __device__ __forceinline__ int bsearch_eq(const float* __restrict__ dom, int card, float x) {
     int lo = 0, hi = card;
     while (lo < hi) {
@@ -119,7 +130,7 @@ __device__ unsigned long long* g_stamps = nullptr;
 #define CBN_STAMP(k)                                                                          \
     do {                                                                                      \
         __builtin_amdgcn_sched_barrier(0);                                                    \
-        unsigned long long _t = __builtin_amdgcn_s_memtime();                                 \
+        unsigned long long _t = __builtin_amdgcn_s_memrealtime(); /* 100 MHz, chip-wide */   \
         if (g_stamps && (threadIdx.x & 63) == 0)                                              \
             g_stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12 + (k)] = _t; \
         __builtin_amdgcn_sched_barrier(0);                                                    \
@@ -447,13 +458,13 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
             // values >= 0: uint order == float order.  The last block to arrive
             // publishes the max and re-arms the plan's staging word + counter,
             // so no memset launch is needed between calls.
-            atomicMax(&sync[0], __float_as_uint(m));
+            atomicMax(&sync[4], __float_as_uint(m));
             __threadfence();
-            const unsigned prev = atomicAdd(&sync[1], 1u);
+            const unsigned prev = atomicAdd(&sync[5], 1u);
             if (prev == gridDim.x - 1) {
                 __threadfence();
-                const unsigned v = atomicExch(&sync[0], 0u);
-                atomicExch(&sync[1], 0u);
+                const unsigned v = atomicExch(&sync[4], 0u);
+                atomicExch(&sync[5], 0u);
                 atomicExch(max_bits, v);
             }
         }
@@ -489,13 +500,20 @@ constexpr int kLoc = 8;
 // round per wave, products kept in registers across an agent-scope grid
 // barrier on the global max (all blocks co-resident: grid <= #CUs, 1 block/CU).
 constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2;
+// plan sync buffer (unsigned words): line 0 = {epoch,max} granule (words 0-1),
+// timeout flag (word 2), two-pass max staging (words 4-5); then per parity
+// 1 + kShards + 1 lines (line 1.. : shards, top).  One 128-B line each.
+constexpr int kShards = 8;
+constexpr int kSyncLine = 32;
+constexpr int kSyncLinesPerParity = kShards + 2;
+constexpr int kSyncWords = kSyncLine * (1 + 2 * kSyncLinesPerParity);
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
 template <int VPL, bool USE_LDS, int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, EvPtrs ev,
              long long Q, int N, int RS, int L, unsigned* __restrict__ sync, int parity,
-             unsigned* __restrict__ max_bits, float* __restrict__ out) {
+             unsigned epoch, unsigned* __restrict__ max_bits, float* __restrict__ out) {
     constexpr bool WRITE = MODE == kModeWrite;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
@@ -516,10 +534,11 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     CBN_STAMP(0);
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
     if (tid < ns) sev[tid] = ev.p[tid];
-    if (MODE == kModeFused && blockIdx.x == 0 && tid == 0) {
-        // re-arm the other parity's words for the next fused launch (nobody uses them now)
-        atomicExch(&sync[4 + 4 * (parity ^ 1)], 0u);
-        atomicExch(&sync[5 + 4 * (parity ^ 1)], 0u);
+    if (MODE == kModeFused && blockIdx.x == 0 && tid < 2 * (kShards + 1)) {
+        // re-arm the other parity's shard/top words for the next fused launch
+        // (nobody uses them during this one)
+        unsigned* other = sync + kSyncLine * (kSyncLinesPerParity * (parity ^ 1) + 1);
+        atomicExch(&other[kSyncLine * (tid >> 1) + (tid & 1)], 0u);
     }
     CBN_STAMP(1);
     __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
@@ -649,13 +668,13 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (tid == 0) {
             float m = 0.f;
             for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
-            atomicMax(&sync[0], __float_as_uint(m));
+            atomicMax(&sync[4], __float_as_uint(m));
             __threadfence();
-            const unsigned prev = atomicAdd(&sync[1], 1u);
+            const unsigned prev = atomicAdd(&sync[5], 1u);
             if (prev == gridDim.x - 1) {
                 __threadfence();
-                const unsigned v = atomicExch(&sync[0], 0u);
-                atomicExch(&sync[1], 0u);
+                const unsigned v = atomicExch(&sync[4], 0u);
+                atomicExch(&sync[5], 0u);
                 atomicExch(max_bits, v);
             }
         }
@@ -667,19 +686,44 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (tid == 0) {
             float m = 0.f;
             for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
-            unsigned* st = sync + 4 + 4 * parity;  // [max bits, arrivals]
-            atomicMax(&st[0], __float_as_uint(m));
-            __threadfence();
-            atomicAdd(&st[1], 1u);
-            unsigned spins = 0;
-            while (__hip_atomic_load(&st[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
-                    atomicOr(&sync[2], 1u);
-                    break;
+            // two-level fan-in (the guide's fanin row: ~12 ns per same-address
+            // atomic): 8 shards on their own 128-B lines take 32 arrivals each in
+            // parallel, the top word takes 8.  Every atomic returns, so a block's
+            // max has landed before its arrival is counted.
+            unsigned* base = sync + kSyncLine * (kSyncLinesPerParity * parity + 1);
+            const unsigned G = gridDim.x;
+            const unsigned sh = blockIdx.x % kShards;
+            const unsigned n_sh = G < kShards ? G : kShards;
+            const unsigned sh_size = (G - sh + kShards - 1) / kShards;
+            unsigned* shl = base + kSyncLine * sh;         // [max, count]
+            unsigned* top = base + kSyncLine * kShards;    // [max, count]
+            unsigned long long* flag = reinterpret_cast<unsigned long long*>(sync);  // line 0: {epoch, max}
+            bool publisher = false;
+            unsigned v = 0;
+            if (atomicMax(&shl[0], __float_as_uint(m)) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
+            if (atomicAdd(&shl[1], 1u) == sh_size - 1) {
+                const unsigned smax = atomic_read_mem(&shl[0]);
+                if (atomicMax(&top[0], smax) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
+                if (atomicAdd(&top[1], 1u) == n_sh - 1) {
+                    v = atomic_read_mem(&top[0]);
+                    __hip_atomic_store(flag, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    publisher = true;
                 }
             }
-            const unsigned v = __hip_atomic_load(&st[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!publisher) {
+                unsigned spins = 0;
+                unsigned long long g;
+                while (((g = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+                       (unsigned long long)epoch) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
+                        atomicOr(&sync[kSyncLine * 0 + 2], 1u);
+                        break;
+                    }
+                }
+                v = (unsigned)g;
+            }
             wmax[0] = __uint_as_float(v);
             if (blockIdx.x == 0) atomicExch(max_bits, v);
         }
@@ -735,6 +779,7 @@ struct cbn_plan {
     int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
     int fused_parity = 0;        // fused launches alternate sync-word pairs
+    unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;
     int fast_blocks_per_cu = 1;
@@ -755,7 +800,7 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE ? kModeWrite : kModeMax>), dim3((unsigned)blocks),
                        dim3(kQueryThreads), p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image,
-                       p->image_floats, ev, Q, p->N, p->RS, L, p->d_sync, 0, max_bits, out);
+                       p->image_floats, ev, Q, p->N, p->RS, L, p->d_sync, 0, 0u, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -769,9 +814,11 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     const long long blocks = (Q + per_block - 1) / per_block;
     const int par = p->fused_parity;
     p->fused_parity ^= 1;
+    const unsigned epoch = ++p->fused_epoch;  // 1, 2, ... (0 = never published)
+    if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeFused>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
-                       p->RS, L, p->d_sync, par, max_bits, out);
+                       p->RS, L, p->d_sync, par, epoch, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -1047,13 +1094,13 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
               hipMalloc(&P->d_slots, sizeof(QSlot) * std::max(ns, 1)) == hipSuccess &&
               hipMalloc(&P->d_build, sizeof(BuildItem) * std::max<size_t>(build.size(), 1)) == hipSuccess &&
               hipMalloc(&P->d_image, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess &&
-              hipMalloc(&P->d_sync, sizeof(unsigned) * 16) == hipSuccess;
+              hipMalloc(&P->d_sync, sizeof(unsigned) * kSyncWords) == hipSuccess;
     ok = ok && hipMemcpy(P->d_fac, fac.data(), sizeof(DevFactor) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && (ns == 0 || hipMemcpy(P->d_slots, qs.data(), sizeof(QSlot) * ns, hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && (build.empty() ||
                 hipMemcpy(P->d_build, build.data(), sizeof(BuildItem) * build.size(), hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && hipMemset(P->d_image, 0, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess;
-    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * 16) == hipSuccess;
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
     for (int sl = 0; ok && sl < ns; ++sl)
         ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
                        hipMemcpyDeviceToDevice) == hipSuccess;

@@ -41,4 +41,15 @@ for k in range(1, 11):
     print(f"  d{k:<2} {names[k]:28s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}  max {d.max():9.0f}")
 tot = st[:, 10] - st[:, 0] if bn.engine.fused else st[:, 7] - st[:, 0]
 tot = tot[tot > 0]
-print("  total per wave: median", np.median(tot), "max", tot.max())
+print("  total per wave: median", np.median(tot), "max", tot.max(), "(units: 10 ns ticks of s_memrealtime)")
+# launch / arrival skew within each XCD (blocks b and b+8 share an XCD, so their s_memtime is comparable)
+full = buf.view(-1, 16, S).cpu().numpy()  # [block, wave, stamp]
+nb = int((full[:, 0, 0] > 0).sum())
+e = np.array([full[b, :, 0].min() for b in range(nb)])
+a = np.array([full[b, :, 7].max() for b in range(nb)])
+t0 = e.min()
+print("block entry (ticks after first): p50 %d p90 %d max %d" % tuple(np.percentile(e - t0, [50, 90, 100])))
+print("block arrival at barrier:        p50 %d p90 %d max %d" % tuple(np.percentile(a - t0, [50, 90, 100])))
+print("per-block entry->arrival:        p50 %d p90 %d max %d" % tuple(np.percentile(a - e, [50, 90, 100])))
+late = np.argsort(e)[-8:]
+print("latest-entering blocks:", late.tolist(), (e[late] - t0).tolist())
