@@ -16,7 +16,11 @@ owns 65 536 queries and the ranks exchange the global max with one RCCL
 all-reduce between the two query passes (distributed.sharded_infer).
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` for the dominant
-kernel (the write pass) from HIP events in the timed region, and
+kernel -- the single-launch fused query kernel at N=1 (the write pass when the
+two-launch path runs) -- timed with HIP events recorded by the library on the
+launch stream inside the timed region; ``roofline.traffic`` = its per-launch
+memory-side bytes from the committed rocprofv3 PMC summary of the same command
+(profiles/<round>_summary.json, tools/profile_summary.py), null when absent;
 ``cpu_baseline`` = the CPU oracle (a restatement of the reference algorithm,
 oracle/ref_infer.py) timed on a bounded sample on this host.
 """
@@ -42,6 +46,22 @@ from continuousbayesiannetwork_amd.distributed import sharded_infer  # noqa: E40
 from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def pmc_traffic(kernel: str):
+    """Per-launch traffic (bytes) of ``kernel`` from the newest committed PMC
+    summary (profiles/rNN_summary.json), with its source; (None, None) if none."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        try:
+            with open(path) as fh:
+                k = json.load(fh).get("kernels", {}).get(kernel, {})
+        except (OSError, ValueError):
+            continue
+        if "traffic_bytes" in k:
+            return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def parse():
@@ -155,12 +175,17 @@ def main():
         n_cols = len(names)  # evidence columns read by the write pass
         bytes_write = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
         achieved = bytes_write / twrite / 1e9
+        vpl = int(os.environ.get("CBN_FAST_VPL", "2"))
+        kname = f"k_query_fast<{vpl}, true, {2 if fused else 1}>"  # <VPL, LDS, MODE 2 fused / 1 write>
+        traffic, tsrc = pmc_traffic(kname)
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                        kernel=("k_query_fast<2,true,fused> (single launch: both passes)" if fused
-                                else "k_query_fast<2,true,write> (write pass)"),
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        kernel=kname + (" (single launch: both passes)" if fused else " (write pass)"),
                         avg_us=round(twrite * 1e6, 2), algorithmic_bytes_per_launch=bytes_write,
                         timed_steps=ntimed)
+        if tsrc:
+            roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
+
         if not fused:
             roofline["max_pass_us"] = round(tmax * 1e6, 2)
 

@@ -101,6 +101,28 @@ def load() -> ctypes.CDLL:
     return _lib
 
 
+_host = None
+HOST_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_cbn_host.so")
+
+
+def load_host():
+    """Load (once) the native host fast path (csrc/host_fast.cpp); raise if not built."""
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_PATH):
+            raise NativeError(f"{HOST_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              "g.build()'`")
+        import importlib.machinery
+        import importlib.util
+
+        loader = importlib.machinery.ExtensionFileLoader("_cbn_host", HOST_PATH)
+        spec = importlib.util.spec_from_file_location("_cbn_host", HOST_PATH, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _host = mod
+    return _host
+
+
 def check(rc: int, what: str):
     if rc != 0:
         msg = load().cbn_last_error().decode(errors="replace")

@@ -112,7 +112,7 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
 class _FastPath:
     """Everything the hot path needs for one cached (target, evidence keys, N)."""
 
-    __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom")
+    __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom", "host", "run_fn", "slot_keys")
 
     def __init__(self, plan: "Plan", device: torch.device, first_key):
         self.plan = plan
@@ -122,6 +122,9 @@ class _FastPath:
         self.max_ptr = plan.max_bits.data_ptr()
         self.lib = _native.load()
         self.tdom = {}
+        self.host = _native.load_host().run  # native per-call checks + output allocation + cbn_plan_run
+        self.run_fn = ctypes.cast(self.lib.cbn_plan_run, ctypes.c_void_p).value
+        self.slot_keys = tuple(plan.slots)
 
 
 class InferenceEngine:
@@ -309,6 +312,16 @@ class InferenceEngine:
         """Hot path: no plan lookup, no context managers, no re-validation
         beyond dtype/device/shape of the evidence columns."""
         plan = fp.plan
+        res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
+                      plan.n_samples, plan.target_observed, fp.max_ptr, self._flags(plan), out)
+        if type(res) is not int:
+            n = res.shape[0]
+            tdom = fp.tdom.get(n)
+            if tdom is None:
+                tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
+            return res, tdom
+        if res > 0:
+            _native.check(res, "cbn_plan_run")
         n = evidence[fp.first].shape[0] if fp.first is not None else 1
         ptrs = fp.ptrs
         for i, v in enumerate(plan.slots):

@@ -25,9 +25,10 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchfast) step bench 600 python bench.py --no-cpu-baseline ;;
     benchcold) step bench_cold 600 python bench.py --no-cpu-baseline --rebuild-tables ;;
-    prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
-    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline &&
-         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    prof) step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline &&
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline ;;
+    summary) step summary 120 python tools/profile_summary.py --tag "${TAG:-r01}" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 40)" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
