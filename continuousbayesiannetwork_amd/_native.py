@@ -68,10 +68,13 @@ _SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "cbn_plan_fused_capacity": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 CBN_RUN_BUILD_TABLES = 1
 CBN_RUN_TIMED = 2
 CBN_RUN_TWO_PASS = 4
+CBN_RUN_RAW = 8
+CBN_E_UNSUPPORTED = -4
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

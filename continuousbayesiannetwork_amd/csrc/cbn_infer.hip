@@ -499,7 +499,11 @@ constexpr int kLoc = 8;
 // MODE 0: max pass, 1: write pass (two launches); 2: fused -- one launch, one
 // round per wave, products kept in registers across an agent-scope grid
 // barrier on the global max (all blocks co-resident: grid <= #CUs, 1 block/CU).
-constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2;
+// MODE 3 (raw): one launch, no grid barrier -- stores the unnormalised
+// products and publishes this launch's max like MODE 0 (the sharded path
+// all-reduces that max across ranks, then k_scale divides in place: the same
+// fp32 division acc / max as the single-launch path, so the rows are identical).
+constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
 // plan sync buffer (unsigned words): line 0 = {epoch,max} granule (words 0-1),
 // timeout flag (word 2), two-pass max staging (words 4-5); then per parity
 // 1 + kShards + 1 lines (line 1.. : shards, top).  One 128-B line each.
@@ -514,7 +518,6 @@ __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, EvPtrs ev,
              long long Q, int N, int RS, int L, unsigned* __restrict__ sync, int parity,
              unsigned epoch, unsigned* __restrict__ max_bits, float* __restrict__ out) {
-    constexpr bool WRITE = MODE == kModeWrite;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
@@ -547,7 +550,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const FastRec* rec = reinterpret_cast<const FastRec*>(img + rec_off);
 
     float maxv = 1.f;
-    if (WRITE) maxv = __uint_as_float(*max_bits);
+    if (MODE == kModeWrite) maxv = __uint_as_float(*max_bits);
     float lmax = 0.f;
     const int qi = lane / L;  // query slot of this lane within the wave
     const int l = lane - qi * L;
@@ -645,12 +648,19 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (first) CBN_STAMP(5);
         if (valid && CBN_OK_OR(q < Q && (long long)(l + 1) * VPL * 4 <= N, 3)) {
             if (MODE == kModeFused) fq = q;
-            if (WRITE) {
+            if (MODE == kModeWrite) {
                 float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
 #pragma unroll
                 for (int v = 0; v < VPL; ++v)
                     o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
                                        acc[4 * v + 3] / maxv);
+            } else if (MODE == kModeRaw) {
+                float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
             } else {
 #pragma unroll
                 for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
@@ -661,7 +671,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         first = false;
     }
     CBN_STAMP(7);
-    if (MODE == kModeMax) {
+    if (MODE == kModeMax || MODE == kModeRaw) {
         lmax = wave_max(lmax);
         if (lane == 0) wmax[wid] = lmax;
         __syncthreads();
@@ -740,6 +750,25 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         }
         CBN_STAMP(10);
     }
+}
+
+// out[i] /= max (bayesian_network.py:296) after a raw launch and the
+// cross-rank all-reduce of the max word; float4 stream, grid-stride.
+__global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_bits) {
+    const float m = __uint_as_float(*max_bits);
+    const long long n4 = n / 4;
+    float4* o4 = reinterpret_cast<float4*>(out);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 v = o4[i];
+        v.x = v.x / m;
+        v.y = v.y / m;
+        v.z = v.z / m;
+        v.w = v.w / m;
+        o4[i] = v;
+    }
+    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = out[i] / m;
 }
 
 int g_num_cu = 0;
@@ -823,6 +852,19 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     return CBN_OK;
 }
 
+template <int VPL>
+int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+    const int L = p->N / (4 * VPL);
+    const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
+    long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL((k_query_fast<VPL, true, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
+                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
+                       p->RS, L, p->d_sync, 0, 0u, max_bits, out);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
 template <int VEC, bool LDS, bool WRITE>
 int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     switch (p->vpl) {
@@ -880,6 +922,12 @@ void allow_lds(size_t bytes) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeFused>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if constexpr (LDS) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, true, kModeRaw>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, true, kModeRaw>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        }
     }
 }
 
@@ -1253,6 +1301,25 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         ++plan->ev_n;
         HIP_TRY(hipEventRecord(e[0], s));
     }
+    if (flags & CBN_RUN_RAW) {
+        if (!plan->fast || !plan->use_lds) return set_err(CBN_E_UNSUPPORTED, "cbn_plan_run: raw launch needs a fast-path plan");
+        if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
+        if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+        if (!plan->d_image || !plan->d_sync) return set_err(CBN_E_ARG, "plan has no device buffers");
+        if (n_queries <= 0) return set_err(CBN_E_ARG, "cbn_plan_run: raw launch needs >= 1 query");
+        EvPtrs ev;
+        memset(&ev, 0, sizeof(ev));
+        for (int i = 0; i < n_evidence; ++i) {
+            if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+            ev.p[i] = evidence[i];
+        }
+        if (e) HIP_TRY(hipEventRecord(e[1], s));
+        rc = plan->vpl == 2 ? launch_raw_v<2>(plan, n_queries, ev, max_bits, out, s)
+                            : launch_raw_v<1>(plan, n_queries, ev, max_bits, out, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[2], s));
+        return CBN_OK;
+    }
     if (n_queries > 0 && !(flags & CBN_RUN_TWO_PASS) && fused_capacity(plan) >= n_queries) {
         // one launch: both passes with the products held in registers across a grid barrier
         if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
@@ -1285,6 +1352,20 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
 }
 
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
+
+int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, void* stream) {
+    if (n < 0 || (n > 0 && (!out || !max_bits))) return set_err(CBN_E_ARG, "cbn_scale: bad arguments");
+    if (n == 0) return CBN_OK;
+    if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_scale: out must be 16-B aligned");
+    long long blocks = (n / 4 + 255) / 256;
+    const long long cap = 4LL * num_cu();
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), out,
+                       (long long)n, max_bits);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
 
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms) {
     if (!plan || !n_timed || !avg_max_ms || !avg_write_ms) return set_err(CBN_E_ARG, "cbn_plan_timing: bad arguments");

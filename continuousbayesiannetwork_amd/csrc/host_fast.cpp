@@ -24,9 +24,9 @@ namespace {
 
 using run_fn = int (*)(void*, int64_t, const float* const*, int32_t, unsigned*, float*, int32_t, hipStream_t);
 
-// Returns (status, out):  status 0 -> out is the result tensor; status -1 -> the
-// fast checks failed (caller takes the slow path); status > 0 -> the C ABI's
-// error code (caller raises with cbn_last_error()).
+// Returns the output tensor; None when a fast check failed (the caller takes
+// the slow path); an int = the C ABI's (negative) error code (the caller
+// raises with cbn_last_error()).
 py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots, py::object first,
                int64_t device_index, int64_t n_samples, bool target_observed, uintptr_t max_ptr, int32_t flags,
                py::object out_obj) {
@@ -34,12 +34,12 @@ py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots,
     int64_t n = 1;
     if (!first.is_none()) {
         PyObject* f = PyDict_GetItem(evidence.ptr(), first.ptr());
-        if (!f || !THPVariable_Check(f)) return py::int_(-1);
+        if (!f || !THPVariable_Check(f)) return py::none();
         const at::Tensor& t = THPVariable_Unpack(f);
-        if (t.dim() < 1) return py::int_(-1);
+        if (t.dim() < 1) return py::none();
         n = t.size(0);
     }
-    if (n == 0 || (!target_observed && n != 1)) return py::int_(-1);
+    if (n == 0 || (!target_observed && n != 1)) return py::none();
     const float* cols_small[64];
     std::vector<const float*> cols_big;
     const float** cols = cols_small;
@@ -49,14 +49,14 @@ py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots,
     }
     for (Py_ssize_t i = 0; i < ns; ++i) {
         PyObject* v = PyDict_GetItem(evidence.ptr(), PyTuple_GET_ITEM(slots.ptr(), i));
-        if (!v || !THPVariable_Check(v)) return py::int_(-1);
+        if (!v || !THPVariable_Check(v)) return py::none();
         const at::Tensor& t = THPVariable_Unpack(v);
         if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != device_index || t.dim() != 2 ||
             t.size(0) != n || !t.is_contiguous())
-            return py::int_(-1);
+            return py::none();
         cols[i] = static_cast<const float*>(t.data_ptr());
     }
-    if (c10::hip::current_device() != device_index) return py::int_(-1);
+    if (c10::hip::current_device() != device_index) return py::none();
     at::Tensor out;
     if (out_obj.is_none()) {
         out = at::empty({n, n_samples}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_index));
@@ -71,9 +71,20 @@ py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots,
     return py::cast(out);
 }
 
+using scale_fn = int (*)(float*, int64_t, const unsigned*, hipStream_t);
+
+// cbn_scale on the current stream of out's device (sharded path, after the
+// cross-rank all-reduce of the max word).
+int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr) {
+    const hipStream_t s = c10::hip::getCurrentHIPStream(out.get_device()).stream();
+    return reinterpret_cast<scale_fn>(fn)(static_cast<float*>(out.data_ptr()), out.numel(),
+                                          reinterpret_cast<const unsigned*>(max_ptr), s);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "cbn MI355X host fast path (cached-plan infer)";
     m.def("run", &run);
+    m.def("scale", &scale);
 }

@@ -45,6 +45,11 @@ def normalise_across_ranks(local_max: Callable[[], torch.Tensor],
     out = local_write(bits)
     if not gather or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return out
+    return gather_rows(out, group, total_rows)
+
+
+def gather_rows(out: torch.Tensor, group=None, total_rows: Optional[int] = None) -> torch.Tensor:
+    """All-gather every rank's [q_r, N] rows (uneven q_r) into the full tensor, rank order."""
     world = dist.get_world_size(group)
     n = out.new_tensor([out.shape[0]], dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(world)]
@@ -67,8 +72,23 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
 
     Each rank passes its own rows of the evidence; the result equals the rows
     of the single-process ``infer`` on the concatenated batch.
+
+    Fast-path plans: ONE launch per rank stores the unnormalised rows and the
+    rank's max word, RCCL all-reduces the word (MAX), and an in-place scale
+    launch divides by the global max.  Other plans: max pass, all-reduce,
+    write pass.
     """
     eng = bn.engine
+    raw = eng.infer_raw(target_node, evidence_shard, N_max, out)
+    if raw is not None:
+        rows, tdom, bits, scale = raw
+        multi = dist.is_initialized() and dist.get_world_size(group) > 1
+        if multi:
+            dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
+        scale(rows, bits)
+        if gather and multi:
+            rows = gather_rows(rows, group)
+        return rows, tdom
     plan, cols, nq, tdom, device = eng.prepare(target_node, evidence_shard, N_max)
     if out is None:
         out = torch.empty((nq, plan.n_samples), dtype=torch.float32, device=device)

@@ -112,7 +112,8 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
 class _FastPath:
     """Everything the hot path needs for one cached (target, evidence keys, N)."""
 
-    __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom", "host", "run_fn", "slot_keys")
+    __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom", "host", "run_fn", "slot_keys",
+                 "scale_fn", "host_scale")
 
     def __init__(self, plan: "Plan", device: torch.device, first_key):
         self.plan = plan
@@ -125,6 +126,8 @@ class _FastPath:
         self.host = _native.load_host().run  # native per-call checks + output allocation + cbn_plan_run
         self.run_fn = ctypes.cast(self.lib.cbn_plan_run, ctypes.c_void_p).value
         self.slot_keys = tuple(plan.slots)
+        self.host_scale = _native.load_host().scale
+        self.scale_fn = ctypes.cast(self.lib.cbn_scale, ctypes.c_void_p).value
 
 
 class InferenceEngine:
@@ -283,6 +286,49 @@ class InferenceEngine:
                 torch.cuda.current_stream(device).synchronize()
                 plan.destroy()
 
+    def infer_raw(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int,
+                  out: Optional[torch.Tensor] = None):
+        """One launch storing this batch's UNnormalised rows (the factor product
+        of bayesian_network.py:269-295) and its max word -- the per-rank step of
+        the sharded path, which all-reduces the word and then calls the returned
+        ``scale(rows, max_bits)`` (the :296 division, in place).
+
+        Returns (rows, target domain, max_bits int32[1], scale) or None when the
+        plan cannot take a raw launch (the caller uses the two-pass exchange).
+        """
+        key = (target, tuple(evidence.keys()), N_max)
+        fp = self._fast.get(key)
+        if fp is None:
+            device = _native.require_gpu(self.bn.device)
+            if len(evidence) == 0:
+                return None
+            observed = relevant_observed(self.bn, self._order(target), evidence.keys())
+            plan = self.plan(target, observed, N_max, device)
+            if not plan.deterministic:
+                plan.destroy()
+                return None
+            fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
+        plan = fp.plan
+        res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
+                      plan.n_samples, plan.target_observed, fp.max_ptr, self._flags(plan) | _native.CBN_RUN_RAW,
+                      out)
+        if res is None or (type(res) is int and res == _native.CBN_E_UNSUPPORTED):
+            return None
+        if type(res) is int:
+            _native.check(res, "cbn_plan_run(raw)")
+        n = res.shape[0]
+        tdom = fp.tdom.get(n)
+        if tdom is None:
+            tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
+
+        def scale(rows: torch.Tensor, bits: torch.Tensor):
+            rc = fp.host_scale(fp.scale_fn, rows, bits.data_ptr())
+            if rc:
+                _native.check(rc, "cbn_scale")
+            return rows
+
+        return res, tdom, plan.max_bits, scale
+
     def _flags(self, plan: Plan) -> int:
         f = 0
         if not (self.cache_tables and plan.tables_built):
@@ -314,14 +360,14 @@ class InferenceEngine:
         plan = fp.plan
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
                       plan.n_samples, plan.target_observed, fp.max_ptr, self._flags(plan), out)
-        if type(res) is not int:
+        if res is not None:
+            if type(res) is int:
+                _native.check(res, "cbn_plan_run")
             n = res.shape[0]
             tdom = fp.tdom.get(n)
             if tdom is None:
                 tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
             return res, tdom
-        if res > 0:
-            _native.check(res, "cbn_plan_run")
         n = evidence[fp.first].shape[0] if fp.first is not None else 1
         ptrs = fp.ptrs
         for i, v in enumerate(plan.slots):

@@ -277,3 +277,45 @@ def test_single_launch_matches_two_launch(Q, gpu):
     if Q <= 64:
         ref, _ = OracleBN(edges, cols, data).infer("X19", {k: v.cpu().numpy() for k, v in ev.items()}, 32)
         np.testing.assert_allclose(b.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("Q,shards", [(1001, 2), (65536, 8), (7, 3)])
+def test_raw_launch_sharded_equals_single_launch(Q, shards, gpu):
+    """Sharded step (one raw launch per shard, MAX of the shards' max words,
+    in-place scale) == the single-process infer, bit for bit."""
+    from continuousbayesiannetwork_amd.distributed import shard_evidence, sharded_infer
+
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    ev = _t(sample_evidence(data, cols, names, Q, 11), gpu)
+    full, _ = bn.infer("X19", ev, N_max=32)
+    full = full.clone()
+    rows, bits, scales = [], [], []
+    for r in range(shards):
+        res = bn.engine.infer_raw("X19", shard_evidence(ev, shards, r), 32)
+        assert res is not None  # fast-path plan takes the raw launch
+        o, _, b, sc = res
+        rows.append(o)
+        bits.append(b.clone())
+        scales.append(sc)
+    m = torch.stack(bits).max(0).values
+    for o, sc in zip(rows, scales):
+        sc(o, m)
+    np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), full.cpu().numpy())
+    # no process group: sharded_infer over the whole batch == infer
+    one, _ = sharded_infer(bn, "X19", ev, N_max=32)
+    np.testing.assert_array_equal(one.cpu().numpy(), full.cpu().numpy())
+
+
+def test_raw_launch_unsupported_plan_falls_back(gpu):
+    """Plans off the fast path (> 32 factors) run the two-pass exchange."""
+    from continuousbayesiannetwork_amd.distributed import sharded_infer
+
+    data, cols, edges = chain_data(40, 3, 4000, 21, stay=0.7)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = _t(sample_evidence(data, cols, ["X38", "X20", "X3"], 900, 4), gpu)
+    assert bn.engine.infer_raw("X39", ev, 3) is None
+    a, _ = bn.infer("X39", ev, N_max=3)
+    b, _ = sharded_infer(bn, "X39", ev, N_max=3)
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())

@@ -41,12 +41,12 @@ def test_argument_errors_are_reported_without_gpu():
 
 def test_host_fast_path_module_rejects_non_device_evidence():
     """The native host fast path loads and hands anything it cannot pass to the
-    C ABI as-is (here: CPU tensors) back to the Python slow path (-1), without
+    C ABI as-is (here: CPU tensors) back to the Python slow path (None), without
     touching the function pointer it was given."""
     import torch
 
     run = _native.load_host().run
     ev = {"a": torch.zeros(8, 1), "b": torch.zeros(8, 1)}
-    assert run(0, 0, ev, ("a", "b"), "a", 0, 4, True, 0, 0, None) == -1
-    assert run(0, 0, ev, ("a", "missing"), "a", 0, 4, True, 0, 0, None) == -1
-    assert run(0, 0, {"a": torch.zeros(0, 1)}, ("a",), "a", 0, 4, True, 0, 0, None) == -1
+    assert run(0, 0, ev, ("a", "b"), "a", 0, 4, True, 0, 0, None) is None
+    assert run(0, 0, ev, ("a", "missing"), "a", 0, 4, True, 0, 0, None) is None
+    assert run(0, 0, {"a": torch.zeros(0, 1)}, ("a",), "a", 0, 4, True, 0, 0, None) is None
