@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must be imported before the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcbn_amd.so")
+LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
 
 CBN_MAX_PARENTS = 8
 CBN_MAX_EVIDENCE = 64

@@ -85,22 +85,25 @@ struct EvPtrs {
     const float* p[CBN_MAX_EVIDENCE];
 };
 
+// Fast path: evidence column of observed parent p of factor f at [f * 4 + p]
+// (nullptr: no such parent), built by the host per call and copied into LDS at
+// kernel entry (during the table fill), so after the fill a lane reaches its
+// evidence with one LDS read instead of record -> slot -> column-pointer hops.
+// Entry [f * 4] is never null and carries tags in its low bits (columns are
+// 4-B aligned): kTagMore = the factor has further observed parents,
+// kTagNone = no observed parent (a valid dummy column, read at row 0), so the
+// first-parent loads of all a lane's factors issue back to back, unbranched.
+constexpr int kFastPtrs = 128;
+constexpr uintptr_t kTagMore = 1, kTagNone = 2;
+struct FPtrs {
+    const float* p[kFastPtrs];
+};
+
 struct ColPtrs {
     const float* dom[kMaxP + 1];
     int card[kMaxP + 1];
     int stride[kMaxP + 1];
 };
-
-// Memory-side read of a counter: a returning atomic add of 0, in asm because
-// LLVM folds an idempotent atomicAdd(p, 0) into an L2-served sc1 load -- and an
-// XCD's L2 copy of a line other XCDs keep adding to can stay stale for microseconds.
-__device__ __forceinline__ unsigned atomic_read_mem(unsigned* p) {
-    unsigned v;
-    const unsigned zero = 0u;
-    asm volatile("global_atomic_add %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
-                 : "=v"(v) : "v"(p), "v"(zero) : "memory");
-    return v;
-}
 
 __device__ __forceinline__ int bsearch_eq(const float* __restrict__ dom, int card, float x) {
     int lo = 0, hi = card;
@@ -504,25 +507,26 @@ constexpr int kLoc = 8;
 // all-reduces that max across ranks, then k_scale divides in place: the same
 // fp32 division acc / max as the single-launch path, so the rows are identical).
 constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
-// plan sync buffer (unsigned words): line 0 = {epoch,max} granule (words 0-1),
-// timeout flag (word 2), two-pass max staging (words 4-5); then per parity
-// 1 + kShards + 1 lines (line 1.. : shards, top).  One 128-B line each.
-constexpr int kShards = 8;
+// plan sync buffer (unsigned words): line 0 = timeout flag (word 2) and the
+// max/raw passes' max staging + arrival counter (words 4-5); from word
+// kSlotWordOff, the fused barrier's slots: block b publishes {epoch, max} in
+// its own 8-byte slot and every block polls all of them.
 constexpr int kSyncLine = 32;
-constexpr int kSyncLinesPerParity = kShards + 2;
-constexpr int kSyncWords = kSyncLine * (1 + 2 * kSyncLinesPerParity);
+constexpr int kMaxSlots = 1024;
+constexpr int kSlotWordOff = kSyncLine;
+constexpr int kSyncWords = kSlotWordOff + 2 * kMaxSlots;
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
 template <int VPL, bool USE_LDS, int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
-k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, EvPtrs ev,
-             long long Q, int N, int RS, int L, unsigned* __restrict__ sync, int parity,
+k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrs fp,
+             long long Q, int N, int RS, int L, unsigned* __restrict__ sync,
              unsigned epoch, unsigned* __restrict__ max_bits, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
-    const float** sev = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // ns pointers
-    int* woffs_all = reinterpret_cast<int*>(sev + CBN_MAX_EVIDENCE);  // per wave: (64 / L) queries x nf4
+    const float** ptab = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // [nf4][4]
+    int* woffs_all = reinterpret_cast<int*>(ptab + kFastPtrs);  // per wave: (64 / L) queries x nf4
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
     const int lane = tid & (kWave - 1);
@@ -536,13 +540,8 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const long long i_end = q1 * L;
     CBN_STAMP(0);
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
-    if (tid < ns) sev[tid] = ev.p[tid];
-    if (MODE == kModeFused && blockIdx.x == 0 && tid < 2 * (kShards + 1)) {
-        // re-arm the other parity's shard/top words for the next fused launch
-        // (nobody uses them during this one)
-        unsigned* other = sync + kSyncLine * (kSyncLinesPerParity * (parity ^ 1) + 1);
-        atomicExch(&other[kSyncLine * (tid >> 1) + (tid & 1)], 0u);
-    }
+    if (tid < kFastPtrs) ptab[tid] = fp.p[tid];
+    (void)ns;
     CBN_STAMP(1);
     __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
     CBN_STAMP(2);
@@ -565,26 +564,36 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         const bool valid = it < i_end;
         const long long q = valid ? it / L : q0;
         float x[kLoc][kFastObs];
+        // first observed parent of each of the lane's factors: all pointer reads,
+        // then all loads (unbranched: entry f*4 is never null)
+        uintptr_t p0[kLoc];
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
             const int f = l + j * L;
-            if (f < nf) {
-                const FastRec& r = rec[f];
+            p0[j] = reinterpret_cast<uintptr_t>(ptab[(f < nf ? f : 0) * kFastObs]);
+        }
 #pragma unroll
-                for (int p = 0; p < kFastObs; ++p) {
-                    if (p < r.n_obs) {
-#ifdef CBN_CHECKED
-                        if (CBN_OK_OR(r.slot[p] >= 0 && r.slot[p] < ns, 1) && CBN_OK_OR(q >= 0 && q < Q, 2))
-                            x[j][p] = gload(sev[r.slot[p]], q);
-                        else
-                            x[j][p] = -1.f;
-#else
-                        x[j][p] = gload(sev[r.slot[p]], q);
-#endif
-                    }
+        for (int j = 0; j < kLoc; ++j) {
+            const float* col = reinterpret_cast<const float*>(p0[j] & ~(kTagMore | kTagNone));
+            x[j][0] = gload(col, (p0[j] & kTagNone) ? 0 : q);
+        }
+#pragma unroll
+        for (int j = 0; j < kLoc; ++j) {
+            const int f = l + j * L;
+            if (f < nf && (p0[j] & kTagMore)) {  // rare: factors with several observed parents
+#pragma unroll
+                for (int p = 1; p < kFastObs; ++p) {
+                    const float* col = ptab[f * kFastObs + p];
+                    if (col) x[j][p] = gload(col, q);
                 }
             }
         }
+#ifdef CBN_CHECKED
+        if (!CBN_OK_OR(q >= 0 && q < Q, 2)) {
+#pragma unroll
+            for (int j = 0; j < kLoc; ++j) x[j][0] = -1.f;
+        }
+#endif
         if (first) CBN_STAMP(3);
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
@@ -693,49 +702,59 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         lmax = wave_max(lmax);
         if (lane == 0) wmax[wid] = lmax;
         __syncthreads();
-        if (tid == 0) {
-            float m = 0.f;
-            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
-            // two-level fan-in (the guide's fanin row: ~12 ns per same-address
-            // atomic): 8 shards on their own 128-B lines take 32 arrivals each in
-            // parallel, the top word takes 8.  Every atomic returns, so a block's
-            // max has landed before its arrival is counted.
-            unsigned* base = sync + kSyncLine * (kSyncLinesPerParity * parity + 1);
-            const unsigned G = gridDim.x;
-            const unsigned sh = blockIdx.x % kShards;
-            const unsigned n_sh = G < kShards ? G : kShards;
-            const unsigned sh_size = (G - sh + kShards - 1) / kShards;
-            unsigned* shl = base + kSyncLine * sh;         // [max, count]
-            unsigned* top = base + kSyncLine * kShards;    // [max, count]
-            unsigned long long* flag = reinterpret_cast<unsigned long long*>(sync);  // line 0: {epoch, max}
-            bool publisher = false;
-            unsigned v = 0;
-            if (atomicMax(&shl[0], __float_as_uint(m)) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
-            if (atomicAdd(&shl[1], 1u) == sh_size - 1) {
-                const unsigned smax = atomic_read_mem(&shl[0]);
-                if (atomicMax(&top[0], smax) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
-                if (atomicAdd(&top[1], 1u) == n_sh - 1) {
-                    v = atomic_read_mem(&top[0]);
-                    __hip_atomic_store(flag, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    publisher = true;
-                }
-            }
-            if (!publisher) {
-                unsigned spins = 0;
-                unsigned long long g;
-                while (((g = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
-                       (unsigned long long)epoch) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
-                        atomicOr(&sync[kSyncLine * 0 + 2], 1u);
-                        break;
+        if (wid == 0) {
+            // Slot barrier: no counters, no re-arming.  One relaxed agent-scope
+            // 8-byte store publishes {epoch, block max} (single-copy atomic, so a
+            // reader sees the old epoch or the new pair, never a mix); wave 0 of
+            // every block then polls the slots it has not yet seen (lane i owns
+            // slots i, i+64, ...) until all G carry this epoch -- one round trip
+            // after the last block arrives instead of a chain of fan-in atomics.
+            const int nw = nthr / kWave;
+            const float bm = wave_max(lane < nw ? wmax[lane] : 0.f);
+            unsigned long long* slots = reinterpret_cast<unsigned long long*>(sync + kSlotWordOff);
+            const unsigned long long tag = (unsigned long long)epoch << 32;
+            if (lane == 0)
+                __hip_atomic_store(&slots[blockIdx.x], tag | __float_as_uint(bm), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const int G = gridDim.x;
+            constexpr int kPer = kMaxSlots / kWave;
+            unsigned gm = 0;
+            unsigned spins = 0;
+            for (;;) {
+                // all of this round's loads in flight before any is consumed (a
+                // per-slot branch would serialise them: one round trip each)
+                unsigned long long v[kPer];
+#pragma unroll
+                for (int k = 0; k < kPer; ++k)
+                    if (k * kWave < G)  // wave-uniform
+                        v[k] = __hip_atomic_load(&slots[min(lane + k * kWave, G - 1)], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                bool done = true;
+#pragma unroll
+                for (int k = 0; k < kPer; ++k) {
+                    if (k * kWave < G) {
+                        const bool here = (v[k] >> 32) == (unsigned long long)epoch;
+                        done &= here;
+                        const unsigned b = here ? (unsigned)v[k] : 0u;
+                        gm = gm > b ? gm : b;
                     }
                 }
-                v = (unsigned)g;
+                if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
+                    if (lane == 0) atomicOr(&sync[2], 1u);
+                    break;
+                }
             }
-            wmax[0] = __uint_as_float(v);
-            if (blockIdx.x == 0) atomicExch(max_bits, v);
+            // non-negative floats: unsigned order == float order
+            for (int o = kWave / 2; o > 0; o >>= 1) {
+                const unsigned t = (unsigned)__shfl_xor((int)gm, o);
+                gm = gm > t ? gm : t;
+            }
+            if (lane == 0) {
+                wmax[0] = __uint_as_float(gm);
+                if (blockIdx.x == 0) atomicExch(max_bits, gm);
+            }
         }
         CBN_STAMP(8);
         __syncthreads();
@@ -801,13 +820,13 @@ struct cbn_plan {
     float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
     unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
     bool fast = false;           // k_query_fast eligible (records live in the image)
+    int fast_slot[kFastPtrs];    // evidence slot of observed parent p of factor f at [f*4+p] (-1: none)
     static constexpr int kRing = 512;
     hipEvent_t ev[kRing][3] = {};  // timing ring (created on first timed call)
     int ev_n = 0;
     int rec_off = 0;             // float offset of the FastRec array in the image
     int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
-    int fused_parity = 0;        // fused launches alternate sync-word pairs
     unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;
@@ -821,6 +840,21 @@ struct cbn_plan {
 
 namespace {
 
+// this call's column pointer of every (factor, observed parent)
+FPtrs fast_ptrs(const cbn_plan* p, const EvPtrs& ev) {
+    FPtrs fp;
+    // dummy for factors with no observed parent: any column of >= 1 row
+    const float* dummy = p->ns > 0 ? ev.p[0] : p->d_image;
+    for (int i = 0; i < kFastPtrs; ++i) fp.p[i] = p->fast_slot[i] >= 0 ? ev.p[p->fast_slot[i]] : nullptr;
+    for (int f = 0; f < kFastPtrs / kFastObs; ++f) {
+        uintptr_t v = reinterpret_cast<uintptr_t>(fp.p[f * kFastObs]);
+        if (!v) v = reinterpret_cast<uintptr_t>(dummy) | kTagNone;
+        if (fp.p[f * kFastObs + 1]) v |= kTagMore;
+        fp.p[f * kFastObs] = reinterpret_cast<const float*>(v);
+    }
+    return fp;
+}
+
 template <int VPL, bool LDS, bool WRITE>
 int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     const int L = p->N / (4 * VPL);
@@ -829,7 +863,7 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE ? kModeWrite : kModeMax>), dim3((unsigned)blocks),
                        dim3(kQueryThreads), p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image,
-                       p->image_floats, ev, Q, p->N, p->RS, L, p->d_sync, 0, 0u, max_bits, out);
+                       p->image_floats, fast_ptrs(p, ev), Q, p->N, p->RS, L, p->d_sync, 0u, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -841,13 +875,11 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     const int L = p->N / (4 * VPL);
     const long long per_block = (long long)(kQueryThreads / kWave) * (kWave / L);
     const long long blocks = (Q + per_block - 1) / per_block;
-    const int par = p->fused_parity;
-    p->fused_parity ^= 1;
     const unsigned epoch = ++p->fused_epoch;  // 1, 2, ... (0 = never published)
     if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeFused>), dim3((unsigned)blocks), dim3(kQueryThreads),
-                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
-                       p->RS, L, p->d_sync, par, epoch, max_bits, out);
+                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
+                       p->RS, L, p->d_sync, epoch, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -859,8 +891,8 @@ int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits,
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query_fast<VPL, true, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
-                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, ev, Q, p->N,
-                       p->RS, L, p->d_sync, 0, 0u, max_bits, out);
+                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
+                       p->RS, L, p->d_sync, 0u, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -934,7 +966,8 @@ void allow_lds(size_t bytes) {
 long long fused_capacity(const cbn_plan* p) {
     if (!p->fast || !p->use_lds || !p->fused_ok) return 0;
     const int L = p->N / (4 * p->vpl);
-    return (long long)num_cu() * (kQueryThreads / kWave) * (kWave / L);
+    const long long blocks = std::min(num_cu(), kMaxSlots);  // one block per CU, one barrier slot each
+    return blocks * (kQueryThreads / kWave) * (kWave / L);
 }
 
 }  // namespace
@@ -1160,8 +1193,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
 
     // fast path eligibility: N % 4 == 0, lanes per query L = N / (4 VPL) a power
     // of two <= 64, <= kLoc factors per lane, <= kFastObs observed parents each
-    bool fast = vec == 4;
+    bool fast = vec == 4 && n_factors * kFastObs <= kFastPtrs;
     std::vector<FastRec> recs(n_factors);
+    for (int& sl : P->fast_slot) sl = -1;
     for (int f = 0; f < n_factors && fast; ++f) {
         FastRec& r = recs[f];
         memset(&r, 0, sizeof(r));
@@ -1173,6 +1207,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 r.card[r.n_obs] = fac[f].parent_card[p] | (qs[sl].dense ? kDenseBit : 0);
                 r.dom_off[r.n_obs] = qs[sl].dom_off;
                 r.slot[r.n_obs] = sl;
+                P->fast_slot[f * kFastObs + r.n_obs] = sl;
                 ++r.n_obs;
             }
         }
@@ -1190,7 +1225,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     }
     if (fast) {
         const int nf4 = (n_factors + 3) & ~3;
-        const size_t side = (size_t)CBN_MAX_EVIDENCE * sizeof(void*) +
+        const size_t side = (size_t)kFastPtrs * sizeof(void*) +
                             (size_t)(kQueryThreads / kWave) * (kWave / Lf) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
         const bool lds_ok = img_bytes + side <= (size_t)kLdsBudget;
         if (!lds_ok && P->use_lds) fast = false;  // keep one LDS mode per plan
