@@ -461,11 +461,12 @@ k_query(const DevFactor* __restrict__ fac, int nf, const QSlot* __restrict__ slo
             // values >= 0: uint order == float order.  The last block to arrive
             // publishes the max and re-arms the plan's staging word + counter,
             // so no memset launch is needed between calls.
-            atomicMax(&sync[4], __float_as_uint(m));
-            __threadfence();
+            // returning device-scope atomics (no fence, ~3.5 us each): this
+            // block's max is performed before its arrival is counted, so the
+            // last arriver's exchange returns every block's contribution
+            if (atomicMax(&sync[4], __float_as_uint(m)) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
             const unsigned prev = atomicAdd(&sync[5], 1u);
             if (prev == gridDim.x - 1) {
-                __threadfence();
                 const unsigned v = atomicExch(&sync[4], 0u);
                 atomicExch(&sync[5], 0u);
                 atomicExch(max_bits, v);
@@ -559,13 +560,12 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     float acc[NV];
     long long fq = -1;  // fused: the one query this lane holds (-1: none)
     // wave-uniform round loop: a wave's 64 items are qpw whole queries
-    for (long long wbase = q0 * L + (long long)wid * kWave; wbase < i_end; wbase += nthr) {
-        const long long it = wbase + lane;
-        const bool valid = it < i_end;
-        const long long q = valid ? it / L : q0;
-        float x[kLoc][kFastObs];
-        // first observed parent of each of the lane's factors: all pointer reads,
-        // then all loads (unbranched: entry f*4 is never null)
+    float x[kLoc][kFastObs];
+    // evidence of round wb into x: first observed parent of each of the lane's
+    // factors -- all pointer reads, then all loads (unbranched: entry f*4 is
+    // never null) -- then the rare further parents
+    auto load_x = [&](long long wb) {
+        const long long q = wb + lane < i_end ? (wb + lane) / L : q0;
         uintptr_t p0[kLoc];
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
@@ -594,6 +594,13 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
             for (int j = 0; j < kLoc; ++j) x[j][0] = -1.f;
         }
 #endif
+    };
+    long long wbase = q0 * L + (long long)wid * kWave;
+    if (wbase < i_end) load_x(wbase);
+    for (; wbase < i_end; wbase += nthr) {
+        const long long it = wbase + lane;
+        const bool valid = it < i_end;
+        const long long q = valid ? it / L : q0;
         if (first) CBN_STAMP(3);
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
@@ -630,6 +637,8 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
         if (first) CBN_STAMP(4);
+        // x is dead: the next round's evidence loads fly during this round's products
+        if (wbase + nthr < i_end) load_x(wbase + nthr);
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         for (int f0 = 0; f0 < nf; f0 += 4) {
@@ -687,11 +696,12 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (tid == 0) {
             float m = 0.f;
             for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
-            atomicMax(&sync[4], __float_as_uint(m));
-            __threadfence();
+            // returning device-scope atomics (no fence, ~3.5 us each): this
+            // block's max is performed before its arrival is counted, so the
+            // last arriver's exchange returns every block's contribution
+            if (atomicMax(&sync[4], __float_as_uint(m)) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
             const unsigned prev = atomicAdd(&sync[5], 1u);
             if (prev == gridDim.x - 1) {
-                __threadfence();
                 const unsigned v = atomicExch(&sync[4], 0u);
                 atomicExch(&sync[5], 0u);
                 atomicExch(max_bits, v);
