@@ -68,7 +68,8 @@ _SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "cbn_plan_fused_capacity": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
-    "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    "cbn_plan_max_words": (ctypes.c_int32, [ctypes.c_void_p]),
 }
 CBN_RUN_BUILD_TABLES = 1
 CBN_RUN_TIMED = 2

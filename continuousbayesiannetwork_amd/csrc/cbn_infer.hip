@@ -126,6 +126,12 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+__device__ __forceinline__ unsigned wave_max_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o, kWave));
+    return v;
+}
+
 // Diagnostic build only (-DCBN_STAMPS): per-wave s_memtime stamps of the query
 // kernels' phases into a debug buffer (never read by the kernels themselves).
 #ifdef CBN_STAMPS
@@ -515,14 +521,19 @@ constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
 constexpr int kSyncLine = 32;
 constexpr int kMaxSlots = 1024;
 constexpr int kSlotWordOff = kSyncLine;
-constexpr int kSyncWords = kSlotWordOff + 2 * kMaxSlots;
+// then the fast max/raw passes' per-block maxima (one word per block; the
+// consumer -- write pass, k_scale, k_reduce_max, or RCCL -- reduces them: no
+// same-address fan-in, ~12 ns per arrival serialised at the memory side)
+constexpr int kMaxWordOff = kSlotWordOff + 2 * kMaxSlots;
+constexpr int kSyncWords = kMaxWordOff + kMaxSlots;
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
 template <int VPL, bool USE_LDS, int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrs fp,
              long long Q, int N, int RS, int L, unsigned* __restrict__ sync,
-             unsigned epoch, unsigned* __restrict__ max_bits, float* __restrict__ out) {
+             unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
+             float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
@@ -550,7 +561,15 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const FastRec* rec = reinterpret_cast<const FastRec*>(img + rec_off);
 
     float maxv = 1.f;
-    if (MODE == kModeWrite) maxv = __uint_as_float(*max_bits);
+    if (MODE == kModeWrite) {
+        // the max pass's per-block maxima (or one all-reduced word): every wave
+        // reduces them itself (L2 hits, no block sync)
+        unsigned m = 0;
+        for (int i = lane; i < n_max; i += kWave) m = max(m, max_in[i]);
+        m = wave_max_u(m);
+        maxv = __uint_as_float(m);
+        if (max_out && blockIdx.x == 0 && tid == 0) *max_out = m;
+    }
     float lmax = 0.f;
     const int qi = lane / L;  // query slot of this lane within the wave
     const int l = lane - qi * L;
@@ -696,17 +715,10 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (tid == 0) {
             float m = 0.f;
             for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
-            // returning device-scope atomics (no fence, ~3.5 us each): this
-            // block's max is performed before its arrival is counted, so the
-            // last arriver's exchange returns every block's contribution
-            if (atomicMax(&sync[4], __float_as_uint(m)) == 0xFFFFFFFFu) atomicOr(&sync[2], 2u);
-            const unsigned prev = atomicAdd(&sync[5], 1u);
-            if (prev == gridDim.x - 1) {
-                const unsigned v = atomicExch(&sync[4], 0u);
-                atomicExch(&sync[5], 0u);
-                atomicExch(max_bits, v);
-            }
+            max_out[blockIdx.x] = __float_as_uint(m);  // one word per block, plain store
         }
+        if (blockIdx.x == 0)  // words of blocks this launch does not have
+            for (int i = (int)gridDim.x + tid; i < n_max; i += nthr) max_out[i] = 0u;
     }
     if (MODE == kModeFused) {
         lmax = wave_max(lmax);
@@ -756,14 +768,10 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                     break;
                 }
             }
-            // non-negative floats: unsigned order == float order
-            for (int o = kWave / 2; o > 0; o >>= 1) {
-                const unsigned t = (unsigned)__shfl_xor((int)gm, o);
-                gm = gm > t ? gm : t;
-            }
+            gm = wave_max_u(gm);  // non-negative floats: unsigned order == float order
             if (lane == 0) {
                 wmax[0] = __uint_as_float(gm);
-                if (blockIdx.x == 0) atomicExch(max_bits, gm);
+                if (blockIdx.x == 0 && max_out) *max_out = gm;
             }
         }
         CBN_STAMP(8);
@@ -783,8 +791,11 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 
 // out[i] /= max (bayesian_network.py:296) after a raw launch and the
 // cross-rank all-reduce of the max word; float4 stream, grid-stride.
-__global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_bits) {
-    const float m = __uint_as_float(*max_bits);
+__global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_in,
+                                               int n_max) {
+    unsigned mb = 0;  // every wave reduces the (all-reduced) per-block maxima itself
+    for (int i = threadIdx.x & (kWave - 1); i < n_max; i += kWave) mb = max(mb, max_in[i]);
+    const float m = __uint_as_float(wave_max_u(mb));
     const long long n4 = n / 4;
     float4* o4 = reinterpret_cast<float4*>(out);
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -798,6 +809,14 @@ __global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long lon
     }
     for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
         out[i] = out[i] / m;
+}
+
+// *out = max of n words (public query_max: per-block maxima -> one word)
+__global__ void __launch_bounds__(64) k_reduce_max(const unsigned* __restrict__ in, int n, unsigned* __restrict__ out) {
+    unsigned m = 0;
+    for (int i = threadIdx.x; i < n; i += kWave) m = max(m, in[i]);
+    m = wave_max_u(m);
+    if (threadIdx.x == 0) *out = m;
 }
 
 int g_num_cu = 0;
@@ -841,6 +860,7 @@ struct cbn_plan {
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;
     int fast_blocks_per_cu = 1;
+    int max_slots = 0;           // fast max/raw passes: blocks per launch at most = words of per-block maxima
     int image_floats = 0;
     int table_floats = 0;
     bool use_lds = false;
@@ -865,15 +885,20 @@ FPtrs fast_ptrs(const cbn_plan* p, const EvPtrs& ev) {
     return fp;
 }
 
+// WRITE=false: per-block maxima -> max_out[0, max_slots); WRITE=true: divide by
+// the max of max_in[0, n_max) (and publish it in *max_out when non-null)
 template <int VPL, bool LDS, bool WRITE>
-int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, const unsigned* max_in, int n_max, unsigned* max_out,
+                  float* out, hipStream_t s) {
     const int L = p->N / (4 * VPL);
-    const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
+    const long long cap = p->max_slots;  // #CUs x blocks per CU, one max word each
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
+    if (!WRITE) n_max = p->max_slots;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE ? kModeWrite : kModeMax>), dim3((unsigned)blocks),
                        dim3(kQueryThreads), p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image,
-                       p->image_floats, fast_ptrs(p, ev), Q, p->N, p->RS, L, p->d_sync, 0u, max_bits, out);
+                       p->image_floats, fast_ptrs(p, ev), Q, p->N, p->RS, L, p->d_sync, 0u, max_in, n_max, max_out,
+                       out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -889,7 +914,7 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeFused>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
-                       p->RS, L, p->d_sync, epoch, max_bits, out);
+                       p->RS, L, p->d_sync, epoch, nullptr, 0, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -897,22 +922,31 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
 template <int VPL>
 int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     const int L = p->N / (4 * VPL);
-    const long long cap = (long long)num_cu() * p->fast_blocks_per_cu;
+    const long long cap = p->max_slots;
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL((k_query_fast<VPL, true, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
-                       p->RS, L, p->d_sync, 0u, max_bits, out);
+                       p->RS, L, p->d_sync, 0u, nullptr, p->max_slots, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
 
+// public pass API on the fast kernel: max pass -> per-block words -> one word
 template <int VEC, bool LDS, bool WRITE>
 int launch_fast(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
-    switch (p->vpl) {
-        case 2: return launch_fast_v<2, LDS, WRITE>(p, Q, ev, max_bits, out, s);
-        default: return launch_fast_v<1, LDS, WRITE>(p, Q, ev, max_bits, out, s);
-    }
+    unsigned* slots = p->d_sync + kMaxWordOff;
+    int rc;
+    if (WRITE)
+        rc = p->vpl == 2 ? launch_fast_v<2, LDS, true>(p, Q, ev, max_bits, 1, nullptr, out, s)
+                         : launch_fast_v<1, LDS, true>(p, Q, ev, max_bits, 1, nullptr, out, s);
+    else
+        rc = p->vpl == 2 ? launch_fast_v<2, LDS, false>(p, Q, ev, nullptr, 0, slots, nullptr, s)
+                         : launch_fast_v<1, LDS, false>(p, Q, ev, nullptr, 0, slots, nullptr, s);
+    if (rc || WRITE) return rc;
+    hipLaunchKernelGGL(k_reduce_max, dim3(1), dim3(kWave), 0, s, slots, p->max_slots, max_bits);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
 }
 
 template <int VEC, bool LDS, bool WRITE>
@@ -1244,6 +1278,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             P->vpl = vpl;
             P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
+            P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
                 hipSuccess) {
                 cbn_plan_destroy(P);
@@ -1379,6 +1414,37 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         if (e) HIP_TRY(hipEventRecord(e[2], s));
         return CBN_OK;
     }
+    if (plan->fast && n_queries > 0) {
+        // two launches: per-block maxima into the plan's words, then the write
+        // pass reduces them itself and publishes the max in *max_bits
+        if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
+        if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+        EvPtrs ev;
+        memset(&ev, 0, sizeof(ev));
+        for (int i = 0; i < n_evidence; ++i) {
+            if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+            ev.p[i] = evidence[i];
+        }
+        unsigned* words = plan->d_sync + kMaxWordOff;
+        const bool lds = plan->use_lds;
+        if (plan->vpl == 2)
+            rc = lds ? launch_fast_v<2, true, false>(plan, n_queries, ev, nullptr, 0, words, nullptr, s)
+                     : launch_fast_v<2, false, false>(plan, n_queries, ev, nullptr, 0, words, nullptr, s);
+        else
+            rc = lds ? launch_fast_v<1, true, false>(plan, n_queries, ev, nullptr, 0, words, nullptr, s)
+                     : launch_fast_v<1, false, false>(plan, n_queries, ev, nullptr, 0, words, nullptr, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[1], s));
+        if (plan->vpl == 2)
+            rc = lds ? launch_fast_v<2, true, true>(plan, n_queries, ev, words, plan->max_slots, max_bits, out, s)
+                     : launch_fast_v<2, false, true>(plan, n_queries, ev, words, plan->max_slots, max_bits, out, s);
+        else
+            rc = lds ? launch_fast_v<1, true, true>(plan, n_queries, ev, words, plan->max_slots, max_bits, out, s)
+                     : launch_fast_v<1, false, true>(plan, n_queries, ev, words, plan->max_slots, max_bits, out, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[2], s));
+        return CBN_OK;
+    }
     rc = cbn_plan_query_max(plan, n_queries, evidence, n_evidence, max_bits, stream);
     if (rc) return rc;
     if (e) HIP_TRY(hipEventRecord(e[1], s));
@@ -1398,8 +1464,10 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
 
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
 
-int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, void* stream) {
-    if (n < 0 || (n > 0 && (!out || !max_bits))) return set_err(CBN_E_ARG, "cbn_scale: bad arguments");
+int32_t cbn_plan_max_words(const cbn_plan* plan) { return plan && plan->fast && plan->use_lds ? plan->max_slots : 0; }
+
+int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, void* stream) {
+    if (n < 0 || n_max < 1 || (n > 0 && (!out || !max_bits))) return set_err(CBN_E_ARG, "cbn_scale: bad arguments");
     if (n == 0) return CBN_OK;
     if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_scale: out must be 16-B aligned");
     long long blocks = (n / 4 + 255) / 256;
@@ -1407,7 +1475,7 @@ int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, void* stream) {
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), out,
-                       (long long)n, max_bits);
+                       (long long)n, max_bits, (int)n_max);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }

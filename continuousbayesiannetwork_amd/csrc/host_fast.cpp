@@ -71,14 +71,14 @@ py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots,
     return py::cast(out);
 }
 
-using scale_fn = int (*)(float*, int64_t, const unsigned*, hipStream_t);
+using scale_fn = int (*)(float*, int64_t, const unsigned*, int32_t, hipStream_t);
 
 // cbn_scale on the current stream of out's device (sharded path, after the
-// cross-rank all-reduce of the max word).
-int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr) {
+// cross-rank all-reduce of the per-block max words).
+int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max) {
     const hipStream_t s = c10::hip::getCurrentHIPStream(out.get_device()).stream();
     return reinterpret_cast<scale_fn>(fn)(static_cast<float*>(out.data_ptr()), out.numel(),
-                                          reinterpret_cast<const unsigned*>(max_ptr), s);
+                                          reinterpret_cast<const unsigned*>(max_ptr), n_max, s);
 }
 
 }  // namespace

@@ -113,7 +113,7 @@ class _FastPath:
     """Everything the hot path needs for one cached (target, evidence keys, N)."""
 
     __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom", "host", "run_fn", "slot_keys",
-                 "scale_fn", "host_scale")
+                 "scale_fn", "host_scale", "words")
 
     def __init__(self, plan: "Plan", device: torch.device, first_key):
         self.plan = plan
@@ -128,6 +128,9 @@ class _FastPath:
         self.slot_keys = tuple(plan.slots)
         self.host_scale = _native.load_host().scale
         self.scale_fn = ctypes.cast(self.lib.cbn_scale, ctypes.c_void_p).value
+        # raw launches: one max word per block of the launch (0: plan has no raw launch)
+        nw = self.lib.cbn_plan_max_words(plan.handle)
+        self.words = torch.zeros(nw, dtype=torch.int32, device=device) if nw > 0 else None
 
 
 class InferenceEngine:
@@ -293,8 +296,9 @@ class InferenceEngine:
         the sharded path, which all-reduces the word and then calls the returned
         ``scale(rows, max_bits)`` (the :296 division, in place).
 
-        Returns (rows, target domain, max_bits int32[1], scale) or None when the
-        plan cannot take a raw launch (the caller uses the two-pass exchange).
+        Returns (rows, target domain, max words int32[W], scale) or None when
+        the plan cannot take a raw launch (the caller uses the two-pass
+        exchange).  The W words are per-block maxima (all-reduce them with MAX).
         """
         key = (target, tuple(evidence.keys()), N_max)
         fp = self._fast.get(key)
@@ -309,9 +313,11 @@ class InferenceEngine:
                 return None
             fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
         plan = fp.plan
+        if fp.words is None:
+            return None
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
-                      plan.n_samples, plan.target_observed, fp.max_ptr, self._flags(plan) | _native.CBN_RUN_RAW,
-                      out)
+                      plan.n_samples, plan.target_observed, fp.words.data_ptr(),
+                      self._flags(plan) | _native.CBN_RUN_RAW, out)
         if res is None or (type(res) is int and res == _native.CBN_E_UNSUPPORTED):
             return None
         if type(res) is int:
@@ -322,12 +328,12 @@ class InferenceEngine:
             tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
 
         def scale(rows: torch.Tensor, bits: torch.Tensor):
-            rc = fp.host_scale(fp.scale_fn, rows, bits.data_ptr())
+            rc = fp.host_scale(fp.scale_fn, rows, bits.data_ptr(), bits.numel())
             if rc:
                 _native.check(rc, "cbn_scale")
             return rows
 
-        return res, tdom, plan.max_bits, scale
+        return res, tdom, fp.words, scale
 
     def _flags(self, plan: Plan) -> int:
         f = 0

@@ -123,10 +123,12 @@ int cbn_plan_infer(cbn_plan* plan, int64_t n_queries, const float* const* eviden
 #define CBN_RUN_TIMED 2
 #define CBN_RUN_TWO_PASS 4  /* force max + write launches (no single-launch grid-barrier path) */
 /* CBN_RUN_RAW: one launch that stores the UNnormalised products in out and
- * this batch's max in *max_bits (the sharded path: the max is all-reduced
- * across ranks, then cbn_scale divides in place -- bayesian_network.py:296
- * over the whole, multi-rank batch).  CBN_E_UNSUPPORTED for plans off the
- * fast path (the caller then uses query_max / all-reduce / query_write). */
+ * this batch's per-block maxima in max_bits[0, cbn_plan_max_words(plan))
+ * (unused words 0).  The sharded path all-reduces those words (MAX) across
+ * ranks, then cbn_scale divides in place by their max -- bayesian_network.py:296
+ * over the whole, multi-rank batch.  CBN_E_UNSUPPORTED for plans off the fast
+ * path (cbn_plan_max_words == 0; the caller then uses query_max / all-reduce /
+ * query_write). */
 #define CBN_RUN_RAW 8
 int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence,
                  int32_t n_evidence, uint32_t* max_bits, float* out, int32_t flags, void* stream);
@@ -137,9 +139,13 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
  * output is then invalid; reads device memory (synchronous). */
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan);
 
-/* out[i] /= float(*max_bits) for i < n (in place, on `stream`): the global-max
- * division of bayesian_network.py:296 after a CBN_RUN_RAW launch. */
-int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, void* stream);
+/* Words of per-block maxima a CBN_RUN_RAW launch writes (0: no raw launch). */
+int32_t cbn_plan_max_words(const cbn_plan* plan);
+
+/* out[i] /= float(max over max_bits[0, n_max)) for i < n (in place, on
+ * `stream`): the global-max division of bayesian_network.py:296 after a
+ * CBN_RUN_RAW launch and the cross-rank all-reduce of its words. */
+int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, void* stream);
 int cbn_plan_status(cbn_plan* plan, int32_t* status);
 
 /* Average device time (ms) of the max and write passes over the timed calls
