@@ -61,3 +61,44 @@ def sample_evidence(data, cols, names, Q, seed, missing_frac=0.0, missing_value=
             v[m, 0] = missing_value
         ev[nm] = v
     return ev
+
+
+def alarm_like_data(S, seed, n=37, d=8, max_parents=4, n_edges=46):
+    """ALARM-shaped synthetic network (BASELINE configs[2]): n nodes, n_edges
+    edges, in-degree <= max_parents, card d.  Edges go from lower to higher
+    index; X_i = (sum_p c_p X_p + c_0) mod d with probability 0.7, else
+    uniform -- every CPT depends on every parent."""
+    rng = np.random.default_rng(seed)
+    parents = {i: [] for i in range(n)}
+    cand = [(a, b) for b in range(1, n) for a in range(b)]
+    rng.shuffle(cand)
+    # a spanning backbone first (every node after X0 gets >= 1 parent), then extra edges
+    for b in range(1, n):
+        parents[b].append(int(rng.integers(max(0, b - 4), b)))
+    extra = n_edges - (n - 1)
+    for b in (n // 3, (2 * n) // 3, n - 2):  # a few 4-parent nodes, as in ALARM
+        while len(parents[b]) < max_parents and extra > 0:
+            a = int(rng.integers(0, b))
+            if a not in parents[b]:
+                parents[b].append(a)
+                extra -= 1
+    for a, b in cand:
+        if extra <= 0:
+            break
+        if a not in parents[b] and len(parents[b]) < max_parents:
+            parents[b].append(a)
+            extra -= 1
+    X = np.zeros((S, n), np.int64)
+    for i in range(n):
+        ps = sorted(parents[i])
+        if not ps:
+            X[:, i] = rng.integers(0, d, S)
+            continue
+        base = np.full(S, int(rng.integers(0, d)))
+        for p in ps:
+            base = base + X[:, p] * int(rng.integers(1, d))
+        keep = rng.random(S) < 0.7
+        X[:, i] = np.where(keep, base % d, rng.integers(0, d, S))
+    cols = [f"X{i}" for i in range(n)]
+    edges = [(f"X{p}", f"X{i}") for i in range(n) for p in sorted(parents[i])]
+    return X.astype(np.float32), cols, edges
