@@ -93,7 +93,7 @@ struct EvPtrs {
 // 4-B aligned): kTagMore = the factor has further observed parents,
 // kTagNone = no observed parent (a valid dummy column, read at row 0), so the
 // first-parent loads of all a lane's factors issue back to back, unbranched.
-constexpr int kFastPtrs = 128;
+constexpr int kFastPtrs = 256;  // 64 factors x 4 observed parents
 constexpr uintptr_t kTagMore = 1, kTagNone = 2;
 struct FPtrs {
     const float* p[kFastPtrs];
@@ -583,12 +583,13 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     // evidence of round wb into x: first observed parent of each of the lane's
     // factors -- all pointer reads, then all loads (unbranched: entry f*4 is
     // never null) -- then the rare further parents
-    auto load_x = [&](long long wb) {
+    // factors are taken in chunks of kLoc*L (one chunk unless nf > 8 L)
+    auto load_x = [&](long long wb, int c0) {
         const long long q = wb + lane < i_end ? (wb + lane) / L : q0;
         uintptr_t p0[kLoc];
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
-            const int f = l + j * L;
+            const int f = c0 + l + j * L;
             p0[j] = reinterpret_cast<uintptr_t>(ptab[(f < nf ? f : 0) * kFastObs]);
         }
 #pragma unroll
@@ -598,7 +599,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         }
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
-            const int f = l + j * L;
+            const int f = c0 + l + j * L;
             if (f < nf && (p0[j] & kTagMore)) {  // rare: factors with several observed parents
 #pragma unroll
                 for (int p = 1; p < kFastObs; ++p) {
@@ -615,15 +616,18 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 #endif
     };
     long long wbase = q0 * L + (long long)wid * kWave;
-    if (wbase < i_end) load_x(wbase);
+    if (wbase < i_end) load_x(wbase, 0);
+    const int chunk = kLoc * L;
     for (; wbase < i_end; wbase += nthr) {
         const long long it = wbase + lane;
         const bool valid = it < i_end;
         const long long q = valid ? it / L : q0;
         if (first) CBN_STAMP(3);
+        for (int c0 = 0; c0 < nf; c0 += chunk) {  // wave-uniform
+        if (c0 > 0) load_x(wbase, c0);
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
-            const int f = l + j * L;
+            const int f = c0 + l + j * L;
             if (f < nf) {
                 const FastRec& r = rec[f];
                 int o = r.table_off;
@@ -651,13 +655,14 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 my[f] = o;
             }
         }
+        }  // chunks
         // the offsets of this query were written by lanes of this same wave:
         // wait for the LDS writes, keep the compiler from reordering around it
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
         if (first) CBN_STAMP(4);
         // x is dead: the next round's evidence loads fly during this round's products
-        if (wbase + nthr < i_end) load_x(wbase + nthr);
+        if (wbase + nthr < i_end) load_x(wbase + nthr, 0);
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         for (int f0 = 0; f0 < nf; f0 += 4) {
@@ -919,13 +924,13 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     return CBN_OK;
 }
 
-template <int VPL>
+template <int VPL, bool LDS>
 int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     const int L = p->N / (4 * VPL);
     const long long cap = p->max_slots;
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((k_query_fast<VPL, true, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
+    hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
                        p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
                        p->RS, L, p->d_sync, 0u, nullptr, p->max_slots, max_bits, out);
     HIP_TRY(hipGetLastError());
@@ -998,17 +1003,15 @@ void allow_lds(size_t bytes) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeFused>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if constexpr (LDS) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, true, kModeRaw>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, true, kModeRaw>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        }
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, kModeRaw>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeRaw>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     }
 }
 
 long long fused_capacity(const cbn_plan* p) {
-    if (!p->fast || !p->use_lds || !p->fused_ok) return 0;
+    if (!p->fast || !p->fused_ok) return 0;
     const int L = p->N / (4 * p->vpl);
     const long long blocks = std::min(num_cu(), kMaxSlots);  // one block per CU, one barrier slot each
     return blocks * (kQueryThreads / kWave) * (kWave / L);
@@ -1263,7 +1266,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         for (int c : {2, 1}) {  // VPL 4 exceeds 128 VGPRs at 1024 threads (spills)
             if (c > want || (N / 4) % c) continue;
             const int Lc = N / (4 * c);
-            if (Lc <= kWave && (kWave % Lc) == 0 && n_factors <= kLoc * Lc) { vpl = c; Lf = Lc; break; }
+            if (Lc <= kWave && (kWave % Lc) == 0) { vpl = c; Lf = Lc; break; }
         }
         fast = vpl > 0;
     }
@@ -1284,15 +1287,23 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
             }
-            if (P->use_lds && !getenv("CBN_NO_FUSED")) {
+            if (!getenv("CBN_NO_FUSED")) {
                 // the grid barrier needs every block resident: check one block per CU fits
+                // (tables in LDS, or -- image beyond LDS -- read from L2/HBM)
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, false, kModeFused>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, false, kModeFused>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
                 int nb = 0;
-                const void* fn = vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>)
-                                          : reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>);
+                const void* fn =
+                    P->use_lds ? (vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>)
+                                           : reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>))
+                               : (vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, false, kModeFused>)
+                                           : reinterpret_cast<const void*>(&k_query_fast<1, false, kModeFused>));
                 if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, P->fast_lds_bytes) ==
                         hipSuccess && nb >= 1)
                     P->fused_ok = true;
@@ -1382,7 +1393,7 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         HIP_TRY(hipEventRecord(e[0], s));
     }
     if (flags & CBN_RUN_RAW) {
-        if (!plan->fast || !plan->use_lds) return set_err(CBN_E_UNSUPPORTED, "cbn_plan_run: raw launch needs a fast-path plan");
+        if (!plan->fast) return set_err(CBN_E_UNSUPPORTED, "cbn_plan_run: raw launch needs a fast-path plan");
         if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
         if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
         if (!plan->d_image || !plan->d_sync) return set_err(CBN_E_ARG, "plan has no device buffers");
@@ -1394,8 +1405,12 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
             ev.p[i] = evidence[i];
         }
         if (e) HIP_TRY(hipEventRecord(e[1], s));
-        rc = plan->vpl == 2 ? launch_raw_v<2>(plan, n_queries, ev, max_bits, out, s)
-                            : launch_raw_v<1>(plan, n_queries, ev, max_bits, out, s);
+        if (plan->use_lds)
+            rc = plan->vpl == 2 ? launch_raw_v<2, true>(plan, n_queries, ev, max_bits, out, s)
+                                : launch_raw_v<1, true>(plan, n_queries, ev, max_bits, out, s);
+        else
+            rc = plan->vpl == 2 ? launch_raw_v<2, false>(plan, n_queries, ev, max_bits, out, s)
+                                : launch_raw_v<1, false>(plan, n_queries, ev, max_bits, out, s);
         if (rc) return rc;
         if (e) HIP_TRY(hipEventRecord(e[2], s));
         return CBN_OK;
@@ -1408,8 +1423,12 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         memset(&ev, 0, sizeof(ev));
         for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
         if (e) HIP_TRY(hipEventRecord(e[1], s));
-        rc = plan->vpl == 2 ? launch_fused_v<2, true>(plan, n_queries, ev, max_bits, out, s)
-                            : launch_fused_v<1, true>(plan, n_queries, ev, max_bits, out, s);
+        if (plan->use_lds)
+            rc = plan->vpl == 2 ? launch_fused_v<2, true>(plan, n_queries, ev, max_bits, out, s)
+                                : launch_fused_v<1, true>(plan, n_queries, ev, max_bits, out, s);
+        else
+            rc = plan->vpl == 2 ? launch_fused_v<2, false>(plan, n_queries, ev, max_bits, out, s)
+                                : launch_fused_v<1, false>(plan, n_queries, ev, max_bits, out, s);
         if (rc) return rc;
         if (e) HIP_TRY(hipEventRecord(e[2], s));
         return CBN_OK;
@@ -1464,7 +1483,7 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
 
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
 
-int32_t cbn_plan_max_words(const cbn_plan* plan) { return plan && plan->fast && plan->use_lds ? plan->max_slots : 0; }
+int32_t cbn_plan_max_words(const cbn_plan* plan) { return plan && plan->fast ? plan->max_slots : 0; }
 
 int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, void* stream) {
     if (n < 0 || n_max < 1 || (n > 0 && (!out || !max_bits))) return set_err(CBN_E_ARG, "cbn_scale: bad arguments");

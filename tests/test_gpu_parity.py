@@ -309,16 +309,49 @@ def test_raw_launch_sharded_equals_single_launch(Q, shards, gpu):
 
 
 def test_raw_launch_unsupported_plan_falls_back(gpu):
-    """Plans off the fast path (> 32 factors) run the two-pass exchange."""
+    """Plans off the fast path (a factor with > 4 observed parents) run the
+    two-pass exchange."""
     from continuousbayesiannetwork_amd.distributed import sharded_infer
 
-    data, cols, edges = chain_data(40, 3, 4000, 21, stay=0.7)
+    data, cols, edges = _star_data(5, 4, 20000, 3)
     bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
-    ev = _t(sample_evidence(data, cols, ["X38", "X20", "X3"], 900, 4), gpu)
-    assert bn.engine.infer_raw("X39", ev, 3) is None
-    a, _ = bn.infer("X39", ev, N_max=3)
-    b, _ = sharded_infer(bn, "X39", ev, N_max=3)
+    ev = _t(sample_evidence(data, cols, [f"P{i}" for i in range(5)], 900, 4), gpu)
+    assert bn.engine.infer_raw("C", ev, 4) is None
+    a, _ = bn.infer("C", ev, N_max=4)
+    b, _ = sharded_infer(bn, "C", ev, N_max=4)
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+@pytest.mark.parametrize("target,Q", [("X35", 262144), ("X35", 1000), ("X36", 262145)])
+def test_alarm_like_single_launch_global_tables(target, Q, gpu):
+    """configs[2]: table image beyond LDS (8^4-row factors) -> the fused kernel
+    reads tables from L2/HBM; it equals the two-launch path bit for bit, and
+    the sharded raw step equals both."""
+    from continuousbayesiannetwork_amd.distributed import shard_evidence
+
+    data, cols, edges = alarm_like_data(50000, 5)
+    names = [c for c in cols if c != target]
+    ev = _t(sample_evidence(data, cols, names, Q, 12), gpu)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    bn.engine.fused = False
+    a, _ = bn.infer(target, ev, N_max=8)
+    a = a.clone()
+    bn.engine.fused = True
+    b, _ = bn.infer(target, ev, N_max=8)
+    b = b.clone()
+    torch.cuda.synchronize()
+    bn.engine.check_status()
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    rows, words, scales = [], [], []
+    for r in range(3):
+        o, _, w, sc = bn.engine.infer_raw(target, shard_evidence(ev, 3, r), 8)
+        rows.append(o)
+        words.append(w.clone())
+        scales.append(sc)
+    m = torch.stack(words).max(0).values
+    for o, sc in zip(rows, scales):
+        sc(o, m)
+    np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), a.cpu().numpy())
 
 
 @pytest.mark.parametrize("target,N,missing", [("X35", 8, 0.0), ("X35", 4, 0.05), ("X36", 8, 0.02)])
