@@ -16,11 +16,20 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
 
+ABI_VERSION = 2
 CBN_MAX_PARENTS = 8
 CBN_MAX_EVIDENCE = 64
 CBN_FACTOR_SCALAR = 0
 CBN_FACTOR_SHARED = 1
 CBN_FACTOR_QUERY = 2
+
+CBN_MAX_LAYERS = 4
+CBN_MAX_WIDTH = 32
+CBN_FAMILY_GAUSS = 1
+CBN_FAMILY_LOGISTIC = 2
+CBN_ACT = {"tanh": 1, "relu": 2, "sigmoid": 3, "leakyrelu": 4, "gelu": 5, "elu": 6}
+CBN_INPUT_FREE = -1
+CBN_INPUT_ONE = -2
 
 _c_float_p = ctypes.POINTER(ctypes.c_float)
 _c_int_p = ctypes.POINTER(ctypes.c_int32)
@@ -39,6 +48,32 @@ class FactorDesc(ctypes.Structure):
         ("node_sample_idx", ctypes.c_void_p),
         ("parent_sample_idx", ctypes.c_void_p),
         ("parent_domain", ctypes.c_void_p * CBN_MAX_PARENTS),
+    ]
+
+
+class ParamModel(ctypes.Structure):
+    """Mirror of ``cbn_param_model`` (include/cbn_amd.h)."""
+
+    _fields_ = [
+        ("family", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("width", ctypes.c_int32 * (CBN_MAX_LAYERS + 1)),
+        ("act", ctypes.c_int32),
+        ("weights", ctypes.c_void_p),
+        ("scale", ctypes.c_float),
+        ("norm", ctypes.c_float),
+    ]
+
+
+class ParamFactor(ctypes.Structure):
+    """Mirror of ``cbn_param_factor`` (include/cbn_amd.h)."""
+
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("input_slot", ctypes.c_int32 * CBN_MAX_PARENTS),
+        ("input_samples", ctypes.c_void_p),
+        ("node_samples", ctypes.c_void_p),
+        ("model", ParamModel),
     ]
 
 
@@ -70,6 +105,10 @@ _SIGNATURES = {
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "cbn_plan_max_words": (ctypes.c_int32, [ctypes.c_void_p]),
+    "cbn_plan_create_param": (ctypes.c_int, [ctypes.POINTER(ParamFactor), ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "cbn_param_eval": (ctypes.c_int, [ctypes.POINTER(ParamModel), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
 }
 CBN_RUN_BUILD_TABLES = 1
 CBN_RUN_TIMED = 2
@@ -99,7 +138,7 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.cbn_abi_version() != 1:
+        if lib.cbn_abi_version() != ABI_VERSION:
             raise NativeError("libcbn_amd.so ABI version mismatch")
         _lib = lib
     return _lib

@@ -140,6 +140,8 @@ class Node:
         """pdf[i, c, v] = P(domains[i, v] | parents_query[i, :, c]) for all i at once."""
         n_start, k, combos = parents_query.shape
         nv = domains.shape[1]
+        if hasattr(self.estimator, "eval_grid"):  # parametric estimators: one kernel call
+            return self.estimator.eval_grid(parents_query, domains)
         if hasattr(self.estimator, "eval_points"):
             pts = torch.empty((n_start, combos, nv, k + 1), dtype=torch.float32, device=parents_query.device)
             pts[..., :k] = parents_query.permute(0, 2, 1).unsqueeze(2).to(torch.float32)

@@ -32,13 +32,15 @@
 #include <string>
 #include <vector>
 
-#include "../../include/cbn_amd.h"
+#include "cbn_internal.h"
+
+using namespace cbn;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int set_err(int code, const char* fmt, ...) {
+int cbn::set_err(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -48,19 +50,7 @@ int set_err(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                     \
-    do {                                                                                  \
-        hipError_t _e = (expr);                                                           \
-        if (_e != hipSuccess)                                                             \
-            return set_err(CBN_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));     \
-    } while (0)
-
-constexpr int kMaxP = CBN_MAX_PARENTS;
-constexpr int kWave = 64;
-constexpr int kQueryThreads = 1024;
-constexpr int kBuildThreads = 256;
-constexpr int kLdsBudget = 160 * 1024;
-
+namespace cbn {
 // Device-side factor descriptor (built once per plan, read with wave-uniform
 // indices so the compiler keeps it on the scalar path).
 struct DevFactor {
@@ -68,9 +58,9 @@ struct DevFactor {
     int n_parents;
     int node_card;
     int n_free;
-    int parent_card[kMaxP];
-    int ev_slot[kMaxP];
-    int cpd_stride[kMaxP];
+    int parent_card[CBN_MAX_PARENTS];
+    int ev_slot[CBN_MAX_PARENTS];
+    int cpd_stride[CBN_MAX_PARENTS];
     const float* cpd;
     const int* node_sample_idx;
     const int* parent_sample_idx;
@@ -80,6 +70,32 @@ struct DevFactor {
     int free_combos; // N^n_free
     int wave_mode;   // build kernel: 1 = one wave per entry (many free combos)
 };
+
+struct QSlot {
+    int dom_off;  // float offset of the sorted domain in the image
+    int card;
+    int dense;    // 1: domain is exactly {0, 1, ..., card-1} -> index = value
+    int pad;
+};
+
+struct BuildItem {
+    int factor;
+    int unit_begin;
+};
+}  // namespace cbn
+
+namespace {
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return set_err(CBN_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));     \
+    } while (0)
+
+constexpr int kMaxP = CBN_MAX_PARENTS;
+constexpr int kQueryThreads = 1024;
+constexpr int kBuildThreads = 256;
 
 struct EvPtrs {
     const float* p[CBN_MAX_EVIDENCE];
@@ -93,7 +109,6 @@ struct EvPtrs {
 // 4-B aligned): kTagMore = the factor has further observed parents,
 // kTagNone = no observed parent (a valid dummy column, read at row 0), so the
 // first-parent loads of all a lane's factors issue back to back, unbranched.
-constexpr int kFastPtrs = 256;  // 64 factors x 4 observed parents
 constexpr uintptr_t kTagMore = 1, kTagNone = 2;
 struct FPtrs {
     const float* p[kFastPtrs];
@@ -269,11 +284,6 @@ __device__ float entry_partial(const DevFactor& d, int entry, int N, int c0, int
     return s;
 }
 
-struct BuildItem {
-    int factor;
-    int unit_begin;
-};
-
 __global__ void __launch_bounds__(kBuildThreads)
 k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ items, int n_items,
                int total_units, int N, int RS, float* __restrict__ image) {
@@ -305,13 +315,6 @@ k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ 
 // Per-factor record staged in LDS for the query prologue.
 constexpr int kFqInts = 4 + 2 * kMaxP;  // img_off, kind, n_obs, pad, obs_slot[], obs_card[]
 constexpr int kUnroll = 4;
-
-struct QSlot {
-    int dom_off;  // float offset of the sorted domain in the image
-    int card;
-    int dense;    // 1: domain is exactly {0, 1, ..., card-1} -> index = value
-    int pad;
-};
 
 __device__ __forceinline__ int slot_index(const float* __restrict__ img, const QSlot& sl, float x) {
     if (sl.dense) {
@@ -514,18 +517,6 @@ constexpr int kLoc = 8;
 // all-reduces that max across ranks, then k_scale divides in place: the same
 // fp32 division acc / max as the single-launch path, so the rows are identical).
 constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
-// plan sync buffer (unsigned words): line 0 = timeout flag (word 2) and the
-// max/raw passes' max staging + arrival counter (words 4-5); from word
-// kSlotWordOff, the fused barrier's slots: block b publishes {epoch, max} in
-// its own 8-byte slot and every block polls all of them.
-constexpr int kSyncLine = 32;
-constexpr int kMaxSlots = 1024;
-constexpr int kSlotWordOff = kSyncLine;
-// then the fast max/raw passes' per-block maxima (one word per block; the
-// consumer -- write pass, k_scale, k_reduce_max, or RCCL -- reduces them: no
-// same-address fan-in, ~12 ns per arrival serialised at the memory side)
-constexpr int kMaxWordOff = kSlotWordOff + 2 * kMaxSlots;
-constexpr int kSyncWords = kMaxWordOff + kMaxSlots;
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
 template <int VPL, bool USE_LDS, int MODE>
@@ -797,10 +788,12 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // out[i] /= max (bayesian_network.py:296) after a raw launch and the
 // cross-rank all-reduce of the max word; float4 stream, grid-stride.
 __global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_in,
-                                               int n_max) {
+                                               int n_max, unsigned* __restrict__ pub) {
     unsigned mb = 0;  // every wave reduces the (all-reduced) per-block maxima itself
     for (int i = threadIdx.x & (kWave - 1); i < n_max; i += kWave) mb = max(mb, max_in[i]);
-    const float m = __uint_as_float(wave_max_u(mb));
+    mb = wave_max_u(mb);
+    if (pub && blockIdx.x == 0 && threadIdx.x == 0) *pub = mb;
+    const float m = __uint_as_float(mb);
     const long long n4 = n / 4;
     float4* o4 = reinterpret_cast<float4*>(out);
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -826,7 +819,9 @@ __global__ void __launch_bounds__(64) k_reduce_max(const unsigned* __restrict__ 
 
 int g_num_cu = 0;
 
-int num_cu() {
+}  // namespace
+
+int cbn::num_cu() {
     if (g_num_cu == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -837,41 +832,15 @@ int num_cu() {
     return g_num_cu;
 }
 
-}  // namespace
-
-struct cbn_plan {
-    int nf = 0;
-    int ns = 0;
-    int N = 0;
-    int vec = 1;
-    int L = 1;
-    int CH = 1;  // queries per block chunk (LDS-sized)
-    DevFactor* d_fac = nullptr;
-    QSlot* d_slots = nullptr;
-    BuildItem* d_build = nullptr;
-    int n_build = 0;
-    int build_units = 0;
-    float* d_image = nullptr;  // [tables | observed-column domains], 16-B padded pieces
-    unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
-    bool fast = false;           // k_query_fast eligible (records live in the image)
-    int fast_slot[kFastPtrs];    // evidence slot of observed parent p of factor f at [f*4+p] (-1: none)
-    static constexpr int kRing = 512;
-    hipEvent_t ev[kRing][3] = {};  // timing ring (created on first timed call)
-    int ev_n = 0;
-    int rec_off = 0;             // float offset of the FastRec array in the image
-    int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
-    int vpl = 1;                 // fast path: float4 chunks of one query row per lane
-    unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
-    bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
-    size_t fast_lds_bytes = 0;
-    int fast_blocks_per_cu = 1;
-    int max_slots = 0;           // fast max/raw passes: blocks per launch at most = words of per-block maxima
-    int image_floats = 0;
-    int table_floats = 0;
-    bool use_lds = false;
-    size_t lds_bytes = 0;
-    int blocks_per_cu = 1;
-};
+int cbn::launch_scale(float* out, long long n, const unsigned* words, int n_words, unsigned* pub, hipStream_t s) {
+    long long blocks = (n / 4 + 255) / 256;
+    const long long cap = 4LL * num_cu();
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, s, out, n, words, n_words, pub);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
 
 namespace {
 
@@ -1334,6 +1303,7 @@ int cbn_plan_destroy(cbn_plan* plan) {
     if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);
     if (plan->d_sync) (void)hipFree(plan->d_sync);
+    if (plan->param) param_destroy(plan->param);
     delete plan;
     return CBN_OK;
 }
@@ -1359,6 +1329,7 @@ int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
 int cbn_plan_query_max(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
                        uint32_t* max_bits, void* stream) {
     if (!plan || !max_bits || n_queries < 0) return set_err(CBN_E_ARG, "cbn_plan_query_max: bad arguments");
+    if (plan->param) return set_err(CBN_E_UNSUPPORTED, "parametric plans run through cbn_plan_run (raw + scale)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (n_queries == 0) {
         HIP_TRY(hipMemsetAsync(max_bits, 0, sizeof(uint32_t), s));
@@ -1371,6 +1342,7 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
                          const uint32_t* max_bits, float* out, void* stream) {
     if (!plan || !max_bits || n_queries < 0 || (n_queries > 0 && !out))
         return set_err(CBN_E_ARG, "cbn_plan_query_write: bad arguments");
+    if (plan->param) return set_err(CBN_E_UNSUPPORTED, "parametric plans run through cbn_plan_run (raw + scale)");
     return dispatch_query<true>(plan, n_queries, evidence, n_evidence, const_cast<uint32_t*>(max_bits), out,
                                 reinterpret_cast<hipStream_t>(stream));
 }
@@ -1380,6 +1352,21 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
     if (!plan) return set_err(CBN_E_ARG, "null plan");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
+    if (plan->param) {
+        hipEvent_t* e = nullptr;
+        if ((flags & CBN_RUN_TIMED) && plan->ev_n < cbn_plan::kRing) {
+            e = plan->ev[plan->ev_n];
+            for (int k = 0; k < 3; ++k)
+                if (!e[k]) HIP_TRY(hipEventCreate(&e[k]));
+            ++plan->ev_n;
+            HIP_TRY(hipEventRecord(e[0], s));
+            HIP_TRY(hipEventRecord(e[1], s));
+        }
+        rc = param_run(plan, n_queries, evidence, n_evidence, max_bits, out, flags, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[2], s));
+        return CBN_OK;
+    }
     if (flags & CBN_RUN_BUILD_TABLES) {
         rc = cbn_plan_build_tables(plan, stream);
         if (rc) return rc;
@@ -1483,20 +1470,16 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
 
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
 
-int32_t cbn_plan_max_words(const cbn_plan* plan) { return plan && plan->fast ? plan->max_slots : 0; }
+int32_t cbn_plan_max_words(const cbn_plan* plan) {
+    if (plan && plan->param) return param_max_words(plan->param);
+    return plan && plan->fast ? plan->max_slots : 0;
+}
 
 int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, void* stream) {
     if (n < 0 || n_max < 1 || (n > 0 && (!out || !max_bits))) return set_err(CBN_E_ARG, "cbn_scale: bad arguments");
     if (n == 0) return CBN_OK;
     if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_scale: out must be 16-B aligned");
-    long long blocks = (n / 4 + 255) / 256;
-    const long long cap = 4LL * num_cu();
-    if (blocks > cap) blocks = cap;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), out,
-                       (long long)n, max_bits, (int)n_max);
-    HIP_TRY(hipGetLastError());
-    return CBN_OK;
+    return launch_scale(out, (long long)n, max_bits, (int)n_max, nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms) {

@@ -1,0 +1,88 @@
+// cbn_internal.h -- internal layout shared by the translation units of
+// libcbn_amd.so (cbn_infer.hip: discrete/table path + C ABI plumbing;
+// cbn_param.hip: parametric CPD path).  Not part of the public C ABI
+// (include/cbn_amd.h).
+#ifndef CBN_INTERNAL_H
+#define CBN_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/cbn_amd.h"
+
+namespace cbn {
+
+constexpr int kWave = 64;
+constexpr int kLdsBudget = 160 * 1024;
+constexpr int kFastPtrs = 256;  // fast table path: 64 factors x 4 observed parents
+
+// plan sync buffer (unsigned words): line 0 = timeout flag (word 2) and the
+// max/raw passes' max staging + arrival counter (words 4-5); from word
+// kSlotWordOff, the fused barrier's slots: block b publishes {epoch, max} in
+// its own 8-byte slot and every block polls all of them.
+constexpr int kSyncLine = 32;
+constexpr int kMaxSlots = 1024;
+constexpr int kSlotWordOff = kSyncLine;
+// then the max/raw passes' per-block maxima (one word per block; the
+// consumer -- write pass, k_scale, k_reduce_max, or RCCL -- reduces them: no
+// same-address fan-in, ~12 ns per arrival serialised at the memory side)
+constexpr int kMaxWordOff = kSlotWordOff + 2 * kMaxSlots;
+constexpr int kSyncWords = kMaxWordOff + kMaxSlots;
+
+struct DevFactor;
+struct QSlot;
+struct BuildItem;
+struct ParamPlan;  // cbn_param.hip
+
+int set_err(int code, const char* fmt, ...);
+int num_cu();
+
+// out[i] /= max(words[0, n_words)) in place on `s`; block 0 also stores that
+// max word in *pub when pub is non-null.
+int launch_scale(float* out, long long n, const unsigned* words, int n_words, unsigned* pub, hipStream_t s);
+
+// parametric plans (cbn_param.hip)
+int param_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+              uint32_t* max_bits, float* out, int32_t flags, hipStream_t s);
+void param_destroy(ParamPlan* pp);
+int param_max_words(const ParamPlan* pp);
+
+}  // namespace cbn
+
+struct cbn_plan {
+    int nf = 0;
+    int ns = 0;
+    int N = 0;
+    int vec = 1;
+    int L = 1;
+    int CH = 1;  // queries per block chunk (LDS-sized)
+    cbn::DevFactor* d_fac = nullptr;
+    cbn::QSlot* d_slots = nullptr;
+    cbn::BuildItem* d_build = nullptr;
+    int n_build = 0;
+    int build_units = 0;
+    float* d_image = nullptr;    // [tables | observed-column domains | records], 16-B padded pieces
+    unsigned* d_sync = nullptr;  // max pass: staging max word + arrival counter
+    bool fast = false;           // k_query_fast eligible (records live in the image)
+    int fast_slot[cbn::kFastPtrs];  // evidence slot of observed parent p of factor f at [f*4+p] (-1: none)
+    static constexpr int kRing = 512;
+    hipEvent_t ev[kRing][3] = {};  // timing ring (created on first timed call)
+    int ev_n = 0;
+    int rec_off = 0;             // float offset of the FastRec array in the image
+    int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
+    int vpl = 1;                 // fast path: float4 chunks of one query row per lane
+    unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
+    bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
+    size_t fast_lds_bytes = 0;
+    int fast_blocks_per_cu = 1;
+    int max_slots = 0;           // fast max/raw passes: blocks per launch at most = words of per-block maxima
+    int image_floats = 0;
+    int table_floats = 0;
+    bool use_lds = false;
+    size_t lds_bytes = 0;
+    int blocks_per_cu = 1;
+    cbn::ParamPlan* param = nullptr;  // parametric-CPD plan (cbn_plan_create_param); table fields unused
+};
+
+#endif  // CBN_INTERNAL_H

@@ -1,0 +1,690 @@
+// cbn_param.hip -- MI355X (gfx950) kernels for the parametric (continuous)
+// CPDs on the inference path of BayesianNetwork.infer:
+//   LinearRegression   (cbn/parameter_learning/linear_regression.py:104-124)
+//   LogisticRegression (cbn/parameter_learning/logistIc_regression.py:70-100)
+//   NeuralNetwork      (cbn/parameter_learning/neural_network.py:99-131)
+// fed through Node.get_prob (cbn/base/node.py:115-204) and the factor loop of
+// bayesian_network.py:269-296.
+//
+// Unlike the BruteForce tables, a parametric factor depends on the evidence
+// VALUES (mu = model(parents)), so nothing per query can be tabulated: the
+// query kernel evaluates, per query and factor, the model and the density at
+// the node's N sample points, averages over the free parents' sample combos
+// (torch.mean over the parent axes) and multiplies into the running product
+// in the reference's factor order.  The work is transcendental-bound (one
+// exp per (query, factor, column)), not HBM-bound.
+//
+// Layout: the plan image (global, read-only) holds per-factor records,
+// weights, sample points and the query-independent factors' rows; a wave's
+// lanes are 64 consecutive queries sharing one column chunk, so every image
+// read is wave-uniform (scalar loads into SGPRs, no LDS, no VGPRs for
+// weights) and the evidence loads are coalesced along the query axis.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "cbn_internal.h"
+
+using namespace cbn;
+
+namespace {
+
+constexpr int kMaxP = CBN_MAX_PARENTS;
+constexpr int kMaxL = CBN_MAX_LAYERS;
+constexpr int kThreads = 256;
+
+#define PHIP_TRY(expr)                                                                    \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return set_err(CBN_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));     \
+    } while (0)
+
+// Model shape (wave-uniform): nn.Linear stack, activation between layers.
+struct MDesc {
+    int n_layers;
+    int act;
+    int width[kMaxL + 1];
+};
+
+// Per-factor record in the plan image (128 B).
+struct alignas(16) PRec {
+    int kind;      // CBN_FACTOR_*
+    int family;    // CBN_FAMILY_*
+    int unit;      // scale == 1 exactly: (x - mu) / 1 == x - mu, skip the division
+    int M;         // free-parent sample combos N^n_free (1: none)
+    MDesc m;       // 7 ints
+    int w_off;     // float offsets in the image: weights, node samples [N],
+    int s_off;     //   free-input samples [width0][N], query-independent row [N]
+    int fs_off;
+    int c_off;
+    float scale;
+    float norm;
+    int in_slot[kMaxP];
+    int pad[7];
+};
+static_assert(sizeof(PRec) == 128, "PRec layout");
+constexpr int kRecFloats = sizeof(PRec) / 4;
+
+struct PEv {
+    const float* p[CBN_MAX_EVIDENCE];
+};
+
+typedef const __attribute__((address_space(1))) float gfloat_t;
+__device__ __forceinline__ float gload(const float* p, long long i) { return ((gfloat_t*)p)[i]; }
+
+__device__ __forceinline__ unsigned wave_max_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o, kWave));
+    return v;
+}
+
+// activation_map of neural_network.py:10-18 (torch CPU formulas)
+__device__ __forceinline__ float act1(int act, float x) {
+    switch (act) {
+        case CBN_ACT_TANH: return tanhf(x);
+        case CBN_ACT_RELU: return x > 0.f ? x : 0.f;
+        case CBN_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+        case CBN_ACT_LEAKYRELU: return x > 0.f ? x : x * 0.01f;
+        case CBN_ACT_GELU: return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+        case CBN_ACT_ELU: return x > 0.f ? x : expm1f(x);
+        default: return x;
+    }
+}
+
+template <int H>
+__device__ __forceinline__ void activate(int act, int w, float (&h)[H]) {
+    switch (act) {  // wave-uniform: one unrolled loop per activation
+        case CBN_ACT_TANH:
+#pragma unroll
+            for (int o = 0; o < H; ++o)
+                if (o < w) h[o] = tanhf(h[o]);
+            break;
+        case CBN_ACT_RELU:
+#pragma unroll
+            for (int o = 0; o < H; ++o) h[o] = h[o] > 0.f ? h[o] : 0.f;
+            break;
+        case CBN_ACT_LEAKYRELU:
+#pragma unroll
+            for (int o = 0; o < H; ++o) h[o] = h[o] > 0.f ? h[o] : h[o] * 0.01f;
+            break;
+        default:
+#pragma unroll
+            for (int o = 0; o < H; ++o)
+                if (o < w) h[o] = act1(act, h[o]);
+            break;
+    }
+}
+
+// mu = model(z): y = W x + b per nn.Linear (dot product first, then the bias:
+// addmm's order), activation after every layer but the last.  HMAX = 0: the
+// linear-model instantiation (n_layers == 1 only).  The first hidden layer
+// lives in registers; further hidden layers (the reference's default is one,
+// neural_network.py:37) go through this thread's LDS scratch `deep`
+// (2 x HMAX floats, stride kThreads), a compact runtime loop.
+template <int HMAX>
+__device__ __forceinline__ float model_mu(const MDesc& m, const float* __restrict__ W, const float (&z)[kMaxP],
+                                          float* deep) {
+    const int n_in = m.width[0];
+    if (HMAX == 0 || m.n_layers == 1) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxP; ++i)
+            if (i < n_in) s = fmaf(W[i], z[i], s);
+        return s + W[n_in];
+    } else {
+        constexpr int H = HMAX > 0 ? HMAX : 1;
+        float h[H];
+        int win = m.width[1];
+        const float* B = W + win * n_in;
+#pragma unroll
+        for (int o = 0; o < H; ++o) {
+            float s = 0.f;
+            if (o < win) {
+#pragma unroll
+                for (int i = 0; i < kMaxP; ++i)
+                    if (i < n_in) s = fmaf(W[o * n_in + i], z[i], s);
+                s = s + B[o];
+            }
+            h[o] = s;
+        }
+        activate<H>(m.act, win, h);
+        W = B + win;
+        if (m.n_layers > 2) {
+            float* src = deep;
+            float* dst = deep + H * kThreads;
+#pragma unroll
+            for (int i = 0; i < H; ++i) src[i * kThreads] = h[i];
+            for (int layer = 1; layer < m.n_layers - 1; ++layer) {
+                const int wo = m.width[layer + 1];
+                const float* Bl = W + wo * win;
+                for (int o = 0; o < wo; ++o) {
+                    float s = 0.f;
+                    for (int i = 0; i < win; ++i) s = fmaf(W[o * win + i], src[i * kThreads], s);
+                    dst[o * kThreads] = act1(m.act, s + Bl[o]);
+                }
+                float* t = src;
+                src = dst;
+                dst = t;
+                W = Bl + wo;
+                win = wo;
+            }
+#pragma unroll
+            for (int i = 0; i < H; ++i) h[i] = i < win ? src[i * kThreads] : 0.f;
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+            if (i < win) s = fmaf(W[i], h[i], s);
+        return s + W[win];
+    }
+}
+
+// Densities, in the reference's fp32 operation order.  UNIT: scale == 1
+// exactly, so (x - mu) / scale == x - mu and the division is skipped.
+template <int FAM, bool UNIT>
+__device__ __forceinline__ float pdf_t(float scale, float norm, float x, float mu) {
+    if (FAM == CBN_FAMILY_GAUSS) {
+        // linear_regression.py:120-123
+        const float t = UNIT ? (x - mu) : (x - mu) / scale;
+        return norm * expf(-0.5f * (t * t));
+    }
+    // logistIc_regression.py:95-99 / neural_network.py:126-130
+    const float d = UNIT ? (x - mu) : (x - mu) / scale;
+    const float e = expf(-d);
+    const float u = 1.f + e;
+    return e / (scale * (u * u));
+}
+
+__device__ __forceinline__ float pdf_eval(int family, bool unit, float scale, float norm, float x, float mu) {
+    if (family == CBN_FAMILY_GAUSS)
+        return unit ? pdf_t<CBN_FAMILY_GAUSS, true>(scale, norm, x, mu) : pdf_t<CBN_FAMILY_GAUSS, false>(scale, norm, x, mu);
+    return unit ? pdf_t<CBN_FAMILY_LOGISTIC, true>(scale, norm, x, mu) : pdf_t<CBN_FAMILY_LOGISTIC, false>(scale, norm, x, mu);
+}
+
+// fx[j] += pdf(S[j]; mu) for the chunk's columns (S, scale, norm wave-uniform)
+template <int NC, int FAM, bool UNIT>
+__device__ __forceinline__ void add_row_t(float (&fx)[NC], const float* __restrict__ S, int ncol, float sc, float nm,
+                                          float mu) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+        if (j < ncol) fx[j] += pdf_t<FAM, UNIT>(sc, nm, S[j], mu);
+}
+
+template <int NC>
+__device__ __forceinline__ void add_row(int mode, float (&fx)[NC], const float* __restrict__ S, int ncol, float sc,
+                                        float nm, float mu) {
+    switch (mode) {
+        case 0: add_row_t<NC, CBN_FAMILY_GAUSS, true>(fx, S, ncol, sc, nm, mu); break;
+        case 1: add_row_t<NC, CBN_FAMILY_GAUSS, false>(fx, S, ncol, sc, nm, mu); break;
+        case 2: add_row_t<NC, CBN_FAMILY_LOGISTIC, true>(fx, S, ncol, sc, nm, mu); break;
+        default: add_row_t<NC, CBN_FAMILY_LOGISTIC, false>(fx, S, ncol, sc, nm, mu); break;
+    }
+}
+
+// Query kernel.  Wave task t -> column chunk l = t / QW (uniform) and the 64
+// consecutive queries (t % QW) * 64 + lane; every lane keeps its NC outputs'
+// running product in registers.  Writes the UNnormalised rows and one max
+// word per block (the global-max division of bayesian_network.py:296 runs
+// after, in k_scale, possibly after a cross-rank all-reduce of the words).
+template <int NC, int HMAX>
+__global__ void __launch_bounds__(kThreads)
+k_param_query(const float* __restrict__ img, int nf, PEv ev, long long Q, int N, int L, long long QW, int n_words,
+              unsigned* __restrict__ max_out, float* __restrict__ out) {
+    const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);
+    extern __shared__ float deep_smem[];  // sized only for models with >= 2 hidden layers
+    float* deep = deep_smem + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wpb = kThreads / kWave;
+    const long long tasks = QW * L;
+    float lmax = 0.f;
+    for (long long t = (long long)blockIdx.x * wpb + threadIdx.x / kWave; t < tasks; t += (long long)gridDim.x * wpb) {
+        const int l = (int)(t / QW);
+        const long long q = (t - (long long)l * QW) * kWave + lane;
+        const bool valid = q < Q;
+        const long long qs = valid ? q : Q - 1;
+        const int col0 = l * NC;
+        const int ncol = min(NC, N - col0);  // wave-uniform
+        float acc[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        for (int f = 0; f < nf; ++f) {
+            const PRec& r = rec[f];
+            if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
+                const float* c = img + r.c_off + col0;
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    if (j < ncol) acc[j] = acc[j] * c[j];
+                continue;
+            }
+            const int n_in = r.m.width[0];
+            float z[kMaxP];
+#pragma unroll
+            for (int i = 0; i < kMaxP; ++i) {
+                z[i] = 0.f;
+                if (i < n_in) {
+                    const int sl = r.in_slot[i];
+                    if (sl >= 0) z[i] = gload(ev.p[sl], qs);
+                    else if (sl == CBN_INPUT_ONE) z[i] = 1.f;
+                }
+            }
+            const float* W = img + r.w_off;
+            const float* S = img + r.s_off + col0;
+            const int mode = (r.family == CBN_FAMILY_GAUSS ? 0 : 2) + (r.unit ? 0 : 1);
+            const float sc = r.scale, nm = r.norm;
+            float fx[NC];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) fx[j] = 0.f;
+            const float* FS = img + r.fs_off;
+            // M == 1 (every parent observed): one pass, x = pdf (a mean over size-1 axes)
+            for (int c = 0; c < r.M; ++c) {
+                int cc = c;  // meshgrid 'ij' order: last free input fastest (node.py:335-375)
+#pragma unroll
+                for (int i = kMaxP - 1; i >= 0; --i) {
+                    if (i < n_in && r.in_slot[i] == CBN_INPUT_FREE) {
+                        const int qd = cc / N;
+                        z[i] = FS[i * N + (cc - qd * N)];
+                        cc = qd;
+                    }
+                }
+                add_row<NC>(mode, fx, S, ncol, sc, nm, model_mu<HMAX>(r.m, W, z, deep));
+            }
+            if (r.M > 1) {
+                const float Mf = (float)r.M;
+#pragma unroll
+                for (int j = 0; j < NC; ++j) fx[j] = fx[j] / Mf;  // torch.mean = sum / count
+            }
+#pragma unroll
+            for (int j = 0; j < NC; ++j) acc[j] = acc[j] * fx[j];
+        }
+        if (valid) {
+            float* o = out + q * N + col0;
+            if ((N & 3) == 0 && (NC & 3) == 0 && ncol == NC) {
+#pragma unroll
+                for (int v = 0; v < NC / 4; ++v)
+                    reinterpret_cast<float4*>(o)[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    if (j < ncol) o[j] = acc[j];
+            }
+            // torch.max propagates NaN (an overflowed logistic density): so does this
+            // max, and as an unsigned word NaN outranks every non-negative float
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+                if (j < ncol) lmax = (acc[j] > lmax || acc[j] != acc[j]) ? acc[j] : lmax;
+        }
+    }
+    // block max -> one word per block (non-negative floats: uint order == float order)
+    __shared__ unsigned wm[kThreads / kWave];
+    const unsigned wmx = wave_max_u(__float_as_uint(lmax));
+    if (lane == 0) wm[threadIdx.x / kWave] = wmx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned m = 0;
+        for (int i = 0; i < wpb; ++i) m = max(m, wm[i]);
+        max_out[blockIdx.x] = m;
+    }
+    if (blockIdx.x == 0)  // words of blocks this launch does not have
+        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += kThreads) max_out[i] = 0u;
+}
+
+// Query-independent factors, once per plan: SHARED x[j] = mean_c pdf(s_j;
+// mu(c)); SCALAR x = mean_j pdf(s_j; mu(1)) replicated over the row.  One
+// block per factor, thread per column.
+template <int HMAX>
+__global__ void __launch_bounds__(kThreads)
+k_param_const(float* __restrict__ img, const int* __restrict__ which, int N) {
+    extern __shared__ float deep_smem[];
+    float* deep = deep_smem + threadIdx.x;
+    const PRec& r = reinterpret_cast<const PRec*>(img)[which[blockIdx.x]];
+    const float* W = img + r.w_off;
+    const float* S = img + r.s_off;
+    const float* FS = img + r.fs_off;
+    float* C = img + r.c_off;
+    const int n_in = r.m.width[0];
+    const bool unit = r.unit != 0;
+    for (int j0 = 0; j0 < N; j0 += blockDim.x) {  // uniform trip count (model uses LDS scratch)
+        const int j = j0 + threadIdx.x;
+        const int js = j < N ? j : N - 1;
+        float s = 0.f;
+        float z[kMaxP];
+#pragma unroll
+        for (int i = 0; i < kMaxP; ++i) z[i] = (i < n_in && r.in_slot[i] == CBN_INPUT_ONE) ? 1.f : 0.f;
+        for (int c = 0; c < r.M; ++c) {
+            int cc = c;
+#pragma unroll
+            for (int i = kMaxP - 1; i >= 0; --i) {
+                if (i < n_in && r.in_slot[i] == CBN_INPUT_FREE) {
+                    const int qd = cc / N;
+                    z[i] = FS[i * N + (cc - qd * N)];
+                    cc = qd;
+                }
+            }
+            s += pdf_eval(r.family, unit, r.scale, r.norm, S[js], model_mu<HMAX>(r.m, W, z, deep));
+        }
+        if (j < N) C[j] = r.kind == CBN_FACTOR_SCALAR ? s : s / (float)r.M;
+    }
+    if (r.kind == CBN_FACTOR_SCALAR) {  // mean over the N sample points (dim 1 of [1, N])
+        __syncthreads();
+        __shared__ float xs;
+        if (threadIdx.x == 0) {
+            float t = 0.f;
+            for (int j = 0; j < N; ++j) t += C[j];
+            xs = t / (float)N;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < N; j += blockDim.x) C[j] = xs;
+    }
+}
+
+// Estimator get_prob: thread per row, mu once, then the row's points.
+template <int HMAX>
+__global__ void __launch_bounds__(kThreads)
+k_param_eval(MDesc m, int family, int unit, float scale, float norm, const float* __restrict__ W,
+             const float* __restrict__ pts, long long n_rows, int n_pts, const float* __restrict__ query, int bias_only,
+             float* __restrict__ out) {
+    extern __shared__ float deep_smem[];
+    float* deep = deep_smem + threadIdx.x;
+    for (long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x; r < n_rows;
+         r += (long long)gridDim.x * blockDim.x) {
+        const int n_in = m.width[0];
+        float mu;
+        if (bias_only) {
+            mu = 0.f + W[m.width[0] * m.width[1]];  // zeros + bias (linear_regression.py:112-117)
+        } else {
+            float z[kMaxP];
+#pragma unroll
+            for (int i = 0; i < kMaxP; ++i) z[i] = i < n_in ? (query ? query[r * n_in + i] : 1.f) : 0.f;
+            mu = model_mu<HMAX>(m, W, z, deep);
+        }
+        for (int v = 0; v < n_pts; ++v)
+            out[r * n_pts + v] = pdf_eval(family, unit != 0, scale, norm, pts[r * n_pts + v], mu);
+    }
+}
+
+int hmax_for(const MDesc& m) {
+    if (m.n_layers == 1) return 0;
+    int w = 0;
+    for (int l = 1; l < m.n_layers; ++l) w = std::max(w, m.width[l]);
+    return w <= 16 ? 16 : 32;
+}
+
+int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const char* what, int idx) {
+    if (h.family != CBN_FAMILY_GAUSS && h.family != CBN_FAMILY_LOGISTIC)
+        return set_err(CBN_E_ARG, "%s %d: bad family %d", what, idx, h.family);
+    if (h.n_layers < 1 || h.n_layers > kMaxL)
+        return set_err(CBN_E_LIMIT, "%s %d: %d layers (1..%d)", what, idx, h.n_layers, kMaxL);
+    if (h.width[0] < 1 || h.width[0] > kMaxP)
+        return set_err(CBN_E_LIMIT, "%s %d: %d model inputs (1..%d)", what, idx, h.width[0], kMaxP);
+    if (h.width[h.n_layers] != 1) return set_err(CBN_E_ARG, "%s %d: the last layer must have 1 output", what, idx);
+    for (int l = 1; l < h.n_layers; ++l)
+        if (h.width[l] < 1 || h.width[l] > CBN_MAX_WIDTH)
+            return set_err(CBN_E_LIMIT, "%s %d: hidden width %d (1..%d)", what, idx, h.width[l], CBN_MAX_WIDTH);
+    if (h.n_layers > 1 && (h.act < CBN_ACT_TANH || h.act > CBN_ACT_ELU))
+        return set_err(CBN_E_ARG, "%s %d: bad activation %d", what, idx, h.act);
+    if (!h.weights) return set_err(CBN_E_ARG, "%s %d: null weights", what, idx);
+    if (!(h.scale > 0.f)) return set_err(CBN_E_ARG, "%s %d: scale must be > 0", what, idx);
+    memset(&m, 0, sizeof(m));
+    m.n_layers = h.n_layers;
+    m.act = h.act;
+    n_weights = 0;
+    for (int l = 0; l <= h.n_layers; ++l) m.width[l] = h.width[l];
+    for (int l = 0; l < h.n_layers; ++l) n_weights += (long long)h.width[l + 1] * (h.width[l] + 1);
+    return CBN_OK;
+}
+
+// LDS scratch of the deep-model path (>= 2 hidden layers): 2 x HMAX floats per thread
+size_t deep_bytes(const MDesc& m, int hmax) {
+    return m.n_layers > 2 ? (size_t)2 * hmax * kThreads * sizeof(float) : 0;
+}
+
+template <typename K>
+void allow_deep(K* k) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 32 * kThreads * (int)sizeof(float));
+}
+
+template <int HMAX>
+void launch_const_t(float* img, const int* which, int n, int N, size_t lds, hipStream_t s) {
+    allow_deep(&k_param_const<HMAX>);
+    hipLaunchKernelGGL(k_param_const<HMAX>, dim3(n), dim3(kThreads), lds, s, img, which, N);
+}
+
+template <int NC, int HMAX>
+void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
+                    unsigned* words, float* out, hipStream_t s);
+
+}  // namespace
+
+namespace cbn {
+struct ParamPlan {
+    int nf = 0;
+    int N = 0;
+    int ns = 0;
+    int nc = 16;     // output columns per lane
+    int L = 1;       // column chunks per query
+    int hmax = 0;    // 0 / 16 / 32
+    size_t deep = 0; // dynamic LDS of the deep-model path
+    int max_slots = 0;
+    float* d_image = nullptr;
+    int* d_which = nullptr;
+    int image_floats = 0;
+};
+}  // namespace cbn
+
+namespace {
+template <int NC, int HMAX>
+void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
+                    unsigned* words, float* out, hipStream_t s) {
+    allow_deep(&k_param_query<NC, HMAX>);
+    hipLaunchKernelGGL((k_param_query<NC, HMAX>), dim3(grid), dim3(kThreads), pp->deep, s, pp->d_image, pp->nf, ev, Q,
+                       pp->N, pp->L, QW, pp->max_slots, words, out);
+}
+
+template <int NC>
+void launch_query_nc(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
+                     unsigned* words, float* out, hipStream_t s) {
+    switch (pp->hmax) {
+        case 0: launch_query_t<NC, 0>(pp, grid, ev, Q, QW, words, out, s); break;
+        case 16: launch_query_t<NC, 16>(pp, grid, ev, Q, QW, words, out, s); break;
+        default: launch_query_t<NC, 32>(pp, grid, ev, Q, QW, words, out, s); break;
+    }
+}
+}  // namespace
+
+void cbn::param_destroy(ParamPlan* pp) {
+    if (!pp) return;
+    if (pp->d_image) (void)hipFree(pp->d_image);
+    if (pp->d_which) (void)hipFree(pp->d_which);
+    delete pp;
+}
+
+int cbn::param_max_words(const ParamPlan* pp) { return pp ? pp->max_slots : 0; }
+
+int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+                   uint32_t* max_bits, float* out, int32_t flags, hipStream_t s) {
+    const ParamPlan* pp = plan->param;
+    if (n_evidence != pp->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", pp->ns, n_evidence);
+    if (n_queries <= 0) return set_err(CBN_E_ARG, "cbn_plan_run: parametric plans need >= 1 query");
+    if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+    if (!pp->d_image || !plan->d_sync) return set_err(CBN_E_ARG, "plan has no device buffers");
+    PEv ev;
+    memset(&ev, 0, sizeof(ev));
+    for (int i = 0; i < n_evidence; ++i) {
+        if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+        ev.p[i] = evidence[i];
+    }
+    const long long QW = (n_queries + kWave - 1) / kWave;
+    const long long waves = QW * pp->L;
+    long long grid = (waves + kThreads / kWave - 1) / (kThreads / kWave);
+    grid = std::max(1LL, std::min(grid, (long long)pp->max_slots));
+    const bool raw = (flags & CBN_RUN_RAW) != 0;
+    unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
+    switch (pp->nc) {
+        case 8: launch_query_nc<8>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
+        case 16: launch_query_nc<16>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
+        default: launch_query_nc<32>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
+    }
+    PHIP_TRY(hipGetLastError());
+    if (raw) return CBN_OK;
+    if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_plan_run: out must be 16-B aligned");
+    return launch_scale(out, n_queries * (long long)pp->N, words, pp->max_slots, max_bits, s);
+}
+
+extern "C" {
+
+int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, int32_t n_samples, cbn_plan** plan) {
+    if (!plan || !factors || n_factors <= 0 || n_samples <= 0)
+        return set_err(CBN_E_ARG, "cbn_plan_create_param: bad arguments");
+    *plan = nullptr;
+    const int N = n_samples;
+    std::vector<PRec> recs(n_factors);
+    std::vector<int> consts;
+    long long off = (long long)n_factors * kRecFloats;
+    int ns = 0, hmax = 0;
+    for (int f = 0; f < n_factors; ++f) {
+        const cbn_param_factor& h = factors[f];
+        PRec& r = recs[f];
+        memset(&r, 0, sizeof(r));
+        long long nw = 0;
+        int rc = check_model(h.model, r.m, nw, "factor", f);
+        if (rc) return rc;
+        hmax = std::max(hmax, hmax_for(r.m));
+        if (h.kind < CBN_FACTOR_SCALAR || h.kind > CBN_FACTOR_QUERY)
+            return set_err(CBN_E_ARG, "factor %d: bad kind %d", f, h.kind);
+        if (!h.node_samples) return set_err(CBN_E_ARG, "factor %d: null node samples", f);
+        int n_obs = 0, n_free = 0;
+        long long M = 1;
+        for (int i = 0; i < r.m.width[0]; ++i) {
+            const int sl = h.input_slot[i];
+            if (sl >= 0) {
+                if (sl >= CBN_MAX_EVIDENCE) return set_err(CBN_E_LIMIT, "factor %d: evidence slot %d", f, sl);
+                ns = std::max(ns, sl + 1);
+                ++n_obs;
+            } else if (sl == CBN_INPUT_FREE) {
+                ++n_free;
+                M *= N;
+                if (M >= (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: too many free-parent combos", f);
+            } else if (sl != CBN_INPUT_ONE) {
+                return set_err(CBN_E_ARG, "factor %d: bad input slot %d", f, sl);
+            }
+            r.in_slot[i] = sl;
+        }
+        if (n_free > 0 && !h.input_samples) return set_err(CBN_E_ARG, "factor %d: free inputs without samples", f);
+        if ((h.kind == CBN_FACTOR_QUERY) != (n_obs > 0))
+            return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
+        if (h.kind == CBN_FACTOR_SCALAR && n_free > 0) return set_err(CBN_E_ARG, "factor %d: SCALAR with free inputs", f);
+        r.kind = h.kind;
+        r.family = h.model.family;
+        r.scale = h.model.scale;
+        r.norm = h.model.norm;
+        r.unit = h.model.scale == 1.f ? 1 : 0;
+        r.M = (int)M;
+        r.w_off = (int)off;
+        off += (nw + 3) & ~3LL;
+        r.s_off = (int)off;
+        off += (N + 3) & ~3;
+        if (n_free > 0) {
+            r.fs_off = (int)off;
+            off += ((long long)r.m.width[0] * N + 3) & ~3LL;
+        }
+        if (h.kind != CBN_FACTOR_QUERY) {
+            r.c_off = (int)off;
+            off += (N + 3) & ~3;
+            consts.push_back(f);
+        }
+        if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "parametric plan image too large");
+    }
+    ParamPlan* pp = new ParamPlan();
+    pp->nf = n_factors;
+    pp->N = N;
+    pp->ns = ns;
+    pp->hmax = hmax;
+    for (const PRec& r : recs) pp->deep = std::max(pp->deep, deep_bytes(r.m, hmax));
+    pp->image_floats = (int)off;
+    // column chunk per lane: whole rows when they fit (the model runs once
+    // per query and factor), else 32-column chunks
+    int nc = 32;
+    if (N <= 8) nc = 8;
+    else if (N <= 16) nc = 16;
+    if (const char* e = getenv("CBN_PARAM_NC")) {
+        const int v = atoi(e);
+        if (v == 8 || v == 16 || v == 32) nc = v;
+    }
+    pp->nc = nc;
+    pp->L = (N + nc - 1) / nc;
+    pp->max_slots = std::min(4 * num_cu(), kMaxSlots);
+    cbn_plan* P = new cbn_plan();
+    P->param = pp;
+    P->nf = n_factors;
+    P->ns = ns;
+    P->N = N;
+    bool ok = hipMalloc(&pp->d_image, sizeof(float) * (size_t)off) == hipSuccess &&
+              hipMalloc(&pp->d_which, sizeof(int) * std::max<size_t>(consts.size(), 1)) == hipSuccess &&
+              hipMalloc(&P->d_sync, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    ok = ok && hipMemset(pp->d_image, 0, sizeof(float) * (size_t)off) == hipSuccess;
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    ok = ok && hipMemcpy(pp->d_image, recs.data(), sizeof(PRec) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && (consts.empty() ||
+                hipMemcpy(pp->d_which, consts.data(), sizeof(int) * consts.size(), hipMemcpyHostToDevice) == hipSuccess);
+    for (int f = 0; ok && f < n_factors; ++f) {
+        const cbn_param_factor& h = factors[f];
+        const PRec& r = recs[f];
+        long long nw = 0;
+        for (int l = 0; l < r.m.n_layers; ++l) nw += (long long)r.m.width[l + 1] * (r.m.width[l] + 1);
+        ok = hipMemcpy(pp->d_image + r.w_off, h.model.weights, sizeof(float) * nw, hipMemcpyDeviceToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(pp->d_image + r.s_off, h.node_samples, sizeof(float) * N, hipMemcpyDeviceToDevice) == hipSuccess;
+        if (ok && r.fs_off)
+            ok = hipMemcpy(pp->d_image + r.fs_off, h.input_samples, sizeof(float) * (size_t)r.m.width[0] * N,
+                           hipMemcpyDeviceToDevice) == hipSuccess;
+    }
+    ok = ok && hipDeviceSynchronize() == hipSuccess;
+    if (ok && !consts.empty()) {
+        switch (hmax) {
+            case 0: launch_const_t<0>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
+            case 16: launch_const_t<16>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
+            default: launch_const_t<32>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
+        }
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    }
+    if (!ok) {
+        cbn_plan_destroy(P);
+        return set_err(CBN_E_HIP, "cbn_plan_create_param: device allocation/upload/build failed");
+    }
+    *plan = P;
+    return CBN_OK;
+}
+
+int cbn_param_eval(const cbn_param_model* model, const float* points, int64_t n_rows, int32_t n_points,
+                   const float* query, int32_t root_bias_only, float* out, void* stream) {
+    if (!model || n_rows < 0 || n_points < 0 || (n_rows > 0 && n_points > 0 && (!points || !out)))
+        return set_err(CBN_E_ARG, "cbn_param_eval: bad arguments");
+    MDesc m;
+    long long nw = 0;
+    int rc = check_model(*model, m, nw, "model", 0);
+    if (rc) return rc;
+    if (root_bias_only && m.n_layers != 1) return set_err(CBN_E_ARG, "cbn_param_eval: bias-only needs a linear model");
+    if (n_rows == 0 || n_points == 0) return CBN_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const long long blocks = std::max(1LL, std::min<long long>((n_rows + kThreads - 1) / kThreads, 8192));
+    const int unit = model->scale == 1.f ? 1 : 0;
+#define CBN_EVAL(H)                                                                                                 \
+    allow_deep(&k_param_eval<H>);                                                                                   \
+    hipLaunchKernelGGL(k_param_eval<H>, dim3((unsigned)blocks), dim3(kThreads), deep_bytes(m, H), s, m, model->family, unit, \
+                       model->scale, model->norm, model->weights, points, (long long)n_rows, (int)n_points, query, \
+                       (int)root_bias_only, out)
+    switch (hmax_for(m)) {
+        case 0: CBN_EVAL(0); break;
+        case 16: CBN_EVAL(16); break;
+        default: CBN_EVAL(32); break;
+    }
+#undef CBN_EVAL
+    PHIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+}  // extern "C"

@@ -173,6 +173,13 @@ class InferenceEngine:
 
     # ---------------------------------------------------------------- plan --
     def _materialise(self, plan: Plan, device: torch.device):
+        ests = [self.bn.nodes_obj[s.node].estimator for s in plan.factors]
+        param = [hasattr(e, "model_desc") for e in ests]
+        if all(param):
+            return self._materialise_param(plan, device)
+        if any(param):
+            raise NotImplementedError("a plan mixing BruteForce tables and parametric estimators is not supported "
+                                      "(the reference fits one estimator type per network)")
         lib = _native.load()
         descs = (_native.FactorDesc * len(plan.factors))()
         keep = []
@@ -211,6 +218,54 @@ class InferenceEngine:
             torch.cuda.current_stream(device).synchronize()  # index arrays ready before the D2D copies
             _native.check(lib.cbn_plan_create(descs, len(plan.factors), N, ctypes.byref(handle)),
                           "cbn_plan_create")
+        plan.handle = handle
+        plan.keep = keep
+        plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def _materialise_param(self, plan: Plan, device: torch.device):
+        """cbn_param_factor per ancestor (include/cbn_amd.h): the estimator's
+        packed model, the input wiring (evidence slot / free parent sampled at
+        sample_domain / constant 1 for roots) and the sample points -- the
+        values Node.get_prob evaluates (node.py:152-193)."""
+        lib = _native.load()
+        descs = (_native.ParamFactor * len(plan.factors))()
+        keep = []
+        slot_of = {v: i for i, v in enumerate(plan.slots)}
+        N = plan.n_samples
+        with torch.cuda.device(device):
+            for f, spec in enumerate(plan.factors):
+                est = self.bn.nodes_obj[spec.node].estimator
+                root = not spec.parents
+                model, w = est.model_desc(root=root, device=device)
+                keep.append(w)
+                d = descs[f]
+                d.kind = spec.kind
+                d.model = model
+                k = int(model.width[0])
+                if root:
+                    for i in range(k):
+                        d.input_slot[i] = _native.CBN_INPUT_ONE
+                else:
+                    if len(spec.parents) != k:
+                        raise _native.NativeError(f"node {spec.node}: model has {k} inputs, {len(spec.parents)} parents")
+                    if k > CBN_MAX_PARENTS:
+                        raise _native.NativeError(f"node {spec.node}: {k} parents > {CBN_MAX_PARENTS}")
+                    samples = torch.zeros((k, N), dtype=torch.float32, device=device)
+                    for i, p in enumerate(spec.parents):
+                        if p in spec.observed:
+                            d.input_slot[i] = slot_of[p]
+                        else:
+                            d.input_slot[i] = _native.CBN_INPUT_FREE
+                            samples[i] = spec.free_samples[p].to(device=device, dtype=torch.float32)
+                    keep.append(samples)
+                    d.input_samples = samples.data_ptr()
+                ns = spec.node_samples.to(device=device, dtype=torch.float32).contiguous()
+                keep.append(ns)
+                d.node_samples = ns.data_ptr()
+            handle = ctypes.c_void_p()
+            torch.cuda.current_stream(device).synchronize()  # sample/weight buffers ready before the D2D copies
+            _native.check(lib.cbn_plan_create_param(descs, len(plan.factors), N, ctypes.byref(handle)),
+                          "cbn_plan_create_param")
         plan.handle = handle
         plan.keep = keep
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)

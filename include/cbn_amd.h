@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define CBN_AMD_ABI_VERSION 1
+#define CBN_AMD_ABI_VERSION 2
 
 #define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
 #define CBN_MAX_EVIDENCE 64  /* distinct evidence columns per query batch        */
@@ -151,6 +151,72 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status);
 /* Average device time (ms) of the max and write passes over the timed calls
  * since the last read; waits for them; resets the ring. */
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms);
+
+/* ------------------------------------------------ parametric CPDs ------
+ * The reference's continuous estimators evaluate a density of the node at its
+ * sample points given a location mu computed from the parents' values:
+ *   GAUSS    : LinearRegression._get_prob (linear_regression.py:104-124)
+ *              pdf = (1 / (sigma * sqrt(2 pi))) * exp(-0.5 * ((x - mu) / sigma)^2)
+ *   LOGISTIC : LogisticRegression._get_prob (logistIc_regression.py:70-100) and
+ *              NeuralNetwork._get_prob (neural_network.py:99-131)
+ *              d = (x - mu) / s;  pdf = exp(-d) / (s * (1 + exp(-d))^2)
+ * mu = an nn.Linear stack: y = W x + b per layer, the activation after every
+ * layer but the last (neural_network.py:45-54); one layer = a linear model. */
+#define CBN_MAX_LAYERS 4     /* nn.Linear layers per model          */
+#define CBN_MAX_WIDTH 32     /* units per hidden layer (reference defaults: 16, 32) */
+#define CBN_FAMILY_GAUSS 1
+#define CBN_FAMILY_LOGISTIC 2
+#define CBN_ACT_TANH 1       /* activation_map of neural_network.py:10-18 */
+#define CBN_ACT_RELU 2
+#define CBN_ACT_SIGMOID 3
+#define CBN_ACT_LEAKYRELU 4  /* negative slope 0.01 (nn.LeakyReLU default) */
+#define CBN_ACT_GELU 5       /* exact (erf) form, nn.GELU default         */
+#define CBN_ACT_ELU 6        /* alpha 1 */
+#define CBN_INPUT_FREE -1    /* input = a free parent: its N sample points (mean over combos) */
+#define CBN_INPUT_ONE -2     /* input = constant 1 (root models: neural_network.py:117-119)  */
+
+typedef struct cbn_param_model {
+    int32_t family;                     /* CBN_FAMILY_*                                  */
+    int32_t n_layers;                   /* 1..CBN_MAX_LAYERS                             */
+    int32_t width[CBN_MAX_LAYERS + 1];  /* width[0] = inputs, width[n_layers] = 1         */
+    int32_t act;                        /* CBN_ACT_* (ignored when n_layers == 1)         */
+    const float* weights;               /* device: per layer W[out][in] row-major, then b[out] */
+    float scale;                        /* sigma = exp(log_sigma) / s = exp(log_scale), fp32 */
+    float norm;                         /* GAUSS: 1 / (sigma * sqrt(2 pi)) as fp32 ops; else 0 */
+} cbn_param_model;
+
+/* One ancestor's factor of BayesianNetwork.infer for a parametric estimator.
+ *   SCALAR (root)      : x = mean_j pdf(s_j; mu(1))                         [1]
+ *   SHARED (no parent observed): x[j] = mean over N^k parent-sample combos c
+ *                        of pdf(s_j; mu(c))                                  [N]
+ *   QUERY              : x[q, j] = mean over the free parents' combos c of
+ *                        pdf(s_j; mu(observed values of query q, c))     [Q, N]
+ * (node.py:115-204 with bayesian_network.py:271-294's mean over parent axes.) */
+typedef struct cbn_param_factor {
+    int32_t kind;                         /* CBN_FACTOR_*                            */
+    int32_t input_slot[CBN_MAX_PARENTS];  /* per model input: evidence column >= 0,
+                                             CBN_INPUT_FREE or CBN_INPUT_ONE          */
+    const float* input_samples;           /* device [width[0]][N]: rows of FREE inputs */
+    const float* node_samples;            /* device [N]: the node's evaluation points  */
+    cbn_param_model model;
+} cbn_param_factor;
+
+/* Plan of one (target, observed set, N_max) over parametric factors, run by
+ * cbn_plan_run (default: one raw launch + an in-place scale; CBN_RUN_RAW: the
+ * raw launch alone, per-block maxima in max_bits[0, cbn_plan_max_words)) and
+ * released by cbn_plan_destroy.  Query-independent factors (SCALAR / SHARED)
+ * are evaluated once here. */
+int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, int32_t n_samples,
+                          cbn_plan** plan);
+
+/* Estimator get_prob: out[r, v] = pdf(points[r, v]; mu(query[r, :])) for
+ * r < n_rows, v < n_points (query = NULL: the model input is the constant
+ * CBN_INPUT_ONE vector, or -- root_bias_only -- mu = the last layer's bias,
+ * LinearRegression's query-free mean, linear_regression.py:112-117).
+ * points [n_rows, n_points], query [n_rows, width[0]], out [n_rows, n_points]:
+ * float32 device, row-major. */
+int cbn_param_eval(const cbn_param_model* model, const float* points, int64_t n_rows, int32_t n_points,
+                   const float* query, int32_t root_bias_only, float* out, void* stream);
 
 #ifdef __cplusplus
 }

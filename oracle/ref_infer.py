@@ -18,6 +18,14 @@ tensor-valued ``random.uniform``), the algorithm of:
 * ``cbn/base/bayesian_network.py:86-102``  get_ancestors
 * ``cbn/base/bayesian_network.py:176-206`` get_pdf
 * ``cbn/base/bayesian_network.py:208-305`` infer (factor product / mean-out / max-normalise)
+* ``cbn/parameter_learning/linear_regression.py:78-96``   LinearRegression._get_prob
+* ``cbn/parameter_learning/logistIc_regression.py:67-98`` LogisticRegression._get_prob
+* ``cbn/parameter_learning/neural_network.py:43-52, 95-124`` NeuralNetwork._build_nn / _get_prob
+
+The parametric estimators are restated for inference only: their fitted
+parameters are inputs (the reference's training loop -- torch autograd + Adam --
+is not restated), taken from the reference-generated fixtures or from the
+model under test.
 
 Parity of this oracle is pinned against golden vectors produced by running the
 reference itself (``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``).
@@ -88,13 +96,86 @@ class OracleBruteForce:
 
 
 # --------------------------------------------------------------------------
+# Parametric estimators (linear_regression.py / logistIc_regression.py /
+# neural_network.py), inference only
+# --------------------------------------------------------------------------
+def _act(name: str, x: np.ndarray) -> np.ndarray:
+    """activation_map of neural_network.py:10-18 (torch formulas, float32)."""
+    x = x.astype(np.float32)
+    if name == "tanh":
+        return np.tanh(x)
+    if name == "relu":
+        return np.where(x > 0, x, np.float32(0)).astype(np.float32)
+    if name == "sigmoid":
+        return (np.float32(1) / (np.float32(1) + np.exp(-x))).astype(np.float32)
+    if name == "leakyrelu":
+        return np.where(x > 0, x, x * np.float32(0.01)).astype(np.float32)
+    if name == "gelu":
+        import math
+        erf = np.vectorize(math.erf, otypes=[np.float64])
+        return (x * np.float32(0.5) * (np.float32(1) + erf(x * np.float32(0.7071067811865476)).astype(np.float32))
+                ).astype(np.float32)
+    if name == "elu":
+        return np.where(x > 0, x, np.expm1(x)).astype(np.float32)
+    raise KeyError(name)
+
+
+class OracleParametric:
+    """Inference-time restatement of the three parametric estimators.
+
+    ``layers`` = [(W [out, in], b [out]), ...] (nn.Linear), ``act`` = the
+    activation between layers, ``log_scale`` = log_sigma (``family`` "gauss",
+    LinearRegression) or log_scale ("logistic": LogisticRegression,
+    NeuralNetwork).  ``root_bias_only``: LinearRegression's query-free mean is
+    its bias (linear_regression.py:84-89); the logistic models evaluate on a
+    ones input (logistIc_regression.py:83-86, neural_network.py:111-114).
+    """
+
+    def __init__(self, family: str, layers, log_scale: float, act: Optional[str] = None,
+                 root_bias_only: bool = False):
+        self.family = family
+        self.layers = [(np.asarray(W, np.float32), np.asarray(b, np.float32)) for W, b in layers]
+        self.log_scale = np.float32(log_scale)
+        self.act = act
+        self.root_bias_only = root_bias_only
+
+    def fit(self, node_data, parents_data):
+        pass  # parameters are given
+
+    def mu(self, q: np.ndarray) -> np.ndarray:
+        h = q.astype(np.float32)
+        for i, (W, b) in enumerate(self.layers):
+            h = (h @ W.T + b).astype(np.float32)
+            if i < len(self.layers) - 1:
+                h = _act(self.act, h)
+        return h
+
+    def get_prob(self, points: np.ndarray, query: Optional[np.ndarray] = None) -> np.ndarray:
+        x = np.asarray(points, np.float32)
+        if query is not None:
+            mu = self.mu(np.asarray(query, np.float32)[..., 0])  # [n, 1]
+        elif self.root_bias_only:
+            mu = (np.zeros((x.shape[0], 1), np.float32) + self.layers[-1][1]).astype(np.float32)
+        else:
+            mu = self.mu(np.ones((x.shape[0], 1), np.float32))
+        s = np.exp(self.log_scale).astype(np.float32)
+        if self.family == "gauss":
+            norm = (np.float32(1) / (s * np.sqrt(np.float32(2 * np.pi)))).astype(np.float32)
+            t = ((x - mu) / s).astype(np.float32)
+            return (norm * np.exp(np.float32(-0.5) * t ** 2)).astype(np.float32)
+        d = ((x - mu) / s).astype(np.float32)
+        e = np.exp(-d).astype(np.float32)
+        return (e / (s * (np.float32(1) + e) ** 2)).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
 # Node (node.py)
 # --------------------------------------------------------------------------
 class OracleNode:
-    def __init__(self, name: str, parents: Sequence[str]):
+    def __init__(self, name: str, parents: Sequence[str], est=None):
         self.name = name
         self.parents = sorted(parents)  # node.py:65
-        self.est = OracleBruteForce()
+        self.est = est if est is not None else OracleBruteForce()
         self.info: Dict[str, list] = {}
 
     def fit(self, node_data: np.ndarray, parents_data: Optional[np.ndarray]):
@@ -201,11 +282,12 @@ class OracleNode:
 # --------------------------------------------------------------------------
 class OracleBN:
     def __init__(self, edges: Sequence[Tuple[str, str]], columns: Sequence[str],
-                 data: np.ndarray, nodes: Optional[Sequence[str]] = None):
+                 data: np.ndarray, nodes: Optional[Sequence[str]] = None, estimators: Optional[Dict] = None):
         """``data`` is [S, n_columns] float32, columns named by ``columns``.
 
         ``nodes`` fixes the DAG node insertion order (bayesian_network.py:31-32
-        iterates ``dag.nodes``); default: the columns order.
+        iterates ``dag.nodes``); default: the columns order.  ``estimators``:
+        node -> fitted OracleParametric (default: BruteForce fitted on data).
         """
         self.dag = nx.DiGraph()
         self.dag.add_nodes_from(list(nodes) if nodes is not None else list(columns))
@@ -214,7 +296,7 @@ class OracleBN:
         self.nodes: Dict[str, OracleNode] = {}
         for n in self.dag.nodes:
             parents = sorted(self.dag.predecessors(n))
-            nd = OracleNode(n, parents)
+            nd = OracleNode(n, parents, (estimators or {}).get(n))
             pdata = np.stack([data[:, col[p]] for p in parents], 0) if parents else None
             nd.fit(data[:, col[n]], pdata)
             self.nodes[n] = nd

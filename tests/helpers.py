@@ -4,12 +4,57 @@ import numpy as np
 import pandas as pd
 
 
-def make_bn(cls, edges, columns, data, device, estimator="brute_force"):
+def make_bn(cls, edges, columns, data, device, estimator="brute_force", config=None):
     dag = nx.DiGraph()
     dag.add_nodes_from(columns)
     dag.add_edges_from(edges)
     df = pd.DataFrame(data, columns=columns)
-    return cls(dag, df, {"estimator_name": estimator}, {"inference_obj": "exact"}, device=device)
+    cfg = {"estimator_name": estimator}
+    cfg.update(config or {})
+    return cls(dag, df, cfg, {"inference_obj": "exact"}, device=device)
+
+
+def param_config(estimator, n_epochs=30, lr=0.05, model=None):
+    """Estimator config in the reference's yaml shape (cbn/conf/parameter_learning)."""
+    cfg = {"estimator_name": estimator, "optimizer": {"name": "Adam", "params": {"lr": lr}},
+           "train": {"n_epochs": n_epochs}}
+    if model is not None:
+        cfg["model"] = model
+    return cfg
+
+
+def mixed_dag_data(S, seed, n=50, max_parents=3, discrete_every=2, card=20, unit=False):
+    """BASELINE configs[3]-shaped network: n nodes, every ``discrete_every``-th
+    node discrete (integer levels 0..card-1; card 20 is the reference's
+    discrete/continuous boundary, cbn/base/__init__.py BASE_MAX_CARDINALITY),
+    the rest continuous linear-Gaussian; in-degree <= max_parents, edges from
+    lower to higher index, X{i-1} -> X{i} always (the last node's ancestors
+    are all the others: an n-factor product per query).  ``unit``:
+    scale every column into [0, 1] (targets the BCE-trained logistic models
+    can fit)."""
+    rng = np.random.default_rng(seed)
+    X = np.zeros((S, n), np.float64)
+    edges = []
+    for i in range(n):
+        k = 0 if i == 0 else int(rng.integers(1, min(i, max_parents) + 1))
+        # backbone parent X{i-1} (every node is an ancestor of the last one) + random extras
+        ps = sorted({i - 1} | set(rng.choice(i, size=k - 1, replace=False).tolist())) if k else []
+        k = len(ps)
+        edges += [(f"X{p}", f"X{i}") for p in ps]
+        z = rng.normal(0, 1, S)
+        for p in ps:
+            col = X[:, p]
+            z = z + rng.uniform(-0.8, 0.8) * (col - col.mean()) / (col.std() + 1e-9)
+        z = z / np.sqrt(1 + 0.3 * k)
+        if i % discrete_every == 1:
+            X[:, i] = np.clip(np.round((z + 2.5) / 5.0 * (card - 1)), 0, card - 1)
+        else:
+            X[:, i] = np.round(z, 3)
+    if unit:
+        lo, hi = X.min(0), X.max(0)
+        X = np.round((X - lo) / (hi - lo), 4)
+    cols = [f"X{i}" for i in range(n)]
+    return X.astype(np.float32), cols, edges
 
 
 def chain_data(n, d, S, seed, values=None, noise=(0.6, 0.3, 0.1), stay=None):

@@ -7,7 +7,7 @@ import random
 import numpy as np
 import pytest
 
-from golden_io import golden_names, load_golden
+from golden_io import golden_names, load_golden, load_param_golden, oracle_estimators, param_golden_names
 from oracle.ref_infer import OracleBN
 
 RTOL, ATOL = 1e-5, 1e-7
@@ -38,3 +38,19 @@ def test_golden_manifest_covers_config0():
     g = load_golden("chain5_d4_q1024_parent")
     assert g["pdf"].shape == (1024, 4)
     assert len(g["meta"]["columns"]) == 5
+
+
+@pytest.mark.parametrize("name", param_golden_names())
+def test_oracle_parametric_matches_reference_golden(name):
+    """LinearRegression / LogisticRegression / NeuralNetwork networks: the
+    oracle, given the reference's fitted parameters, reproduces the reference's
+    infer output (NaN where the reference's logistic density overflows)."""
+    g = load_param_golden(name)
+    m = g["meta"]
+    bn = OracleBN(m["edges"], m["columns"], g["data"], estimators=oracle_estimators(g))
+    random.seed(m["seed"])
+    ev = {k: g["evidence"][k] for k in m["evidence"]}
+    pdf, dom = bn.infer(m["target"], ev, m["N_max"])
+    assert pdf.shape == g["pdf"].shape
+    np.testing.assert_array_equal(dom, g["domain"])
+    np.testing.assert_allclose(pdf, g["pdf"], rtol=RTOL, atol=ATOL)
