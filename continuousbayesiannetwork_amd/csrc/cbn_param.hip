@@ -34,7 +34,10 @@ namespace {
 
 constexpr int kMaxP = CBN_MAX_PARENTS;
 constexpr int kMaxL = CBN_MAX_LAYERS;
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;   // const / eval kernels
+constexpr int kQThreads = 512;  // query kernel: 8 waves per block, so the <= 1024-block grid holds 8 waves per SIMD
+constexpr int kColPad = 32;
+constexpr int kInputNone = -3;  // unused model input slot (reads the {0, 1} cell)  // sample / constant rows padded to the widest column chunk
 
 #define PHIP_TRY(expr)                                                                    \
     do {                                                                                  \
@@ -64,7 +67,9 @@ struct alignas(16) PRec {
     float scale;
     float norm;
     int in_slot[kMaxP];
-    int pad[7];
+    float inv_scale;  // fp32 1 / scale (Newton-refined division by the scale)
+    int free_mask;    // bit i: model input i is a free parent (sampled per combo)
+    int pad[5];
 };
 static_assert(sizeof(PRec) == 128, "PRec layout");
 constexpr int kRecFloats = sizeof(PRec) / 4;
@@ -125,7 +130,7 @@ __device__ __forceinline__ void activate(int act, int w, float (&h)[H]) {
 // lives in registers; further hidden layers (the reference's default is one,
 // neural_network.py:37) go through this thread's LDS scratch `deep`
 // (2 x HMAX floats, stride kThreads), a compact runtime loop.
-template <int HMAX>
+template <int HMAX, int STRIDE = kThreads>
 __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restrict__ W, const float (&z)[kMaxP],
                                           float* deep) {
     const int n_in = m.width[0];
@@ -155,16 +160,16 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
         W = B + win;
         if (m.n_layers > 2) {
             float* src = deep;
-            float* dst = deep + H * kThreads;
+            float* dst = deep + H * STRIDE;
 #pragma unroll
-            for (int i = 0; i < H; ++i) src[i * kThreads] = h[i];
+            for (int i = 0; i < H; ++i) src[i * STRIDE] = h[i];
             for (int layer = 1; layer < m.n_layers - 1; ++layer) {
                 const int wo = m.width[layer + 1];
                 const float* Bl = W + wo * win;
                 for (int o = 0; o < wo; ++o) {
                     float s = 0.f;
-                    for (int i = 0; i < win; ++i) s = fmaf(W[o * win + i], src[i * kThreads], s);
-                    dst[o * kThreads] = act1(m.act, s + Bl[o]);
+                    for (int i = 0; i < win; ++i) s = fmaf(W[o * win + i], src[i * STRIDE], s);
+                    dst[o * STRIDE] = act1(m.act, s + Bl[o]);
                 }
                 float* t = src;
                 src = dst;
@@ -173,7 +178,7 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
                 win = wo;
             }
 #pragma unroll
-            for (int i = 0; i < H; ++i) h[i] = i < win ? src[i * kThreads] : 0.f;
+            for (int i = 0; i < H; ++i) h[i] = i < win ? src[i * STRIDE] : 0.f;
         }
         float s = 0.f;
 #pragma unroll
@@ -183,122 +188,212 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
     }
 }
 
-// Densities, in the reference's fp32 operation order.  UNIT: scale == 1
-// exactly, so (x - mu) / scale == x - mu and the division is skipped.
-template <int FAM, bool UNIT>
-__device__ __forceinline__ float pdf_t(float scale, float norm, float x, float mu) {
-    if (FAM == CBN_FAMILY_GAUSS) {
-        // linear_regression.py:120-123
-        const float t = UNIT ? (x - mu) : (x - mu) / scale;
-        return norm * expf(-0.5f * (t * t));
+// n / d to within one ulp of the correctly rounded quotient: v_rcp_f32 + one
+// Newton step (4 VALU slots instead of the ~12 of the IEEE division
+// sequence).  v_rcp_f32 flushes reciprocals below 2^-126, so denominators
+// above 2^126 (a logistic (1 + e)^2 near FLT_MAX), inf and NaN take the IEEE
+// division -- a branch no lane takes in range, skipped by the whole wave.
+__device__ __forceinline__ float div_nr(float n, float d, float r) {
+    const float q = n * r;
+    float res = fmaf(fmaf(-d, q, n), r, q);
+    if (!(d <= 0x1p126f)) res = n / d;
+    return res;
+}
+__device__ __forceinline__ float div_nr(float n, float d) { return div_nr(n, d, __builtin_amdgcn_rcpf(d)); }
+
+// exp(x) within ~2 ulp for results >= 2^-126 in 7 VALU slots (libm expf: 13):
+// x log2(e) = hi + lo exactly (product residual by fma, plus x times the
+// low part of log2(e)), 2^hi by v_exp_f32, 2^lo ~ 1 + lo ln2 (|lo| <= 2^-24
+// |hi|).  x below -104 (exp underflows) is clamped so the residual stays
+// finite; NaN passes through (comparisons false).  v_exp_f32 returns 0 where
+// 2^hi is subnormal (hi < -126): such a density is < 1.2e-38 and flushes to
+// 0 (the reference keeps the subnormal) -- measured and bounded in
+// tests/test_gpu_param.py::test_density_accuracy_full_range.
+__device__ __forceinline__ float exp_split(float x) {
+    constexpr float kL = 1.44269502162933349609375f;  // fp32(log2 e)
+    constexpr float kLlo = 1.925963033500e-8f;       // log2 e - kL
+    constexpr float kLn2 = 0.693147180559945309f;
+    x = x < -104.f ? -104.f : x;
+    const float ph = x * kL;
+    const float pl = fmaf(x, kLlo, fmaf(x, kL, -ph));
+    const float r = __builtin_amdgcn_exp2f(ph);
+    return fmaf(r, pl * kLn2, r);
+}
+
+// Densities, in the reference's fp32 operation order (divisions within one
+// ulp, see div_nr; exp within ~2 ulp, see exp_split).  MODE: 0 Gauss with scale 1, 1 Gauss, 2 logistic with
+// scale 1, 3 logistic.  With scale == 1 exactly, (x - mu) / scale == x - mu.
+template <int MODE>
+__device__ __forceinline__ float pdf_t(float scale, float inv_scale, float norm, float x, float mu) {
+    if (MODE <= 1) {
+        // linear_regression.py:91-95
+        const float t = MODE == 0 ? (x - mu) : div_nr(x - mu, scale, inv_scale);
+        return norm * exp_split(-0.5f * (t * t));
     }
-    // logistIc_regression.py:95-99 / neural_network.py:126-130
-    const float d = UNIT ? (x - mu) : (x - mu) / scale;
-    const float e = expf(-d);
+    // logistIc_regression.py:90-98 / neural_network.py:120-124
+    const float d = MODE == 2 ? (x - mu) : div_nr(x - mu, scale, inv_scale);
+    const float e = exp_split(-d);
     const float u = 1.f + e;
-    return e / (scale * (u * u));
+    return div_nr(e, MODE == 2 ? u * u : scale * (u * u));
 }
 
-__device__ __forceinline__ float pdf_eval(int family, bool unit, float scale, float norm, float x, float mu) {
-    if (family == CBN_FAMILY_GAUSS)
-        return unit ? pdf_t<CBN_FAMILY_GAUSS, true>(scale, norm, x, mu) : pdf_t<CBN_FAMILY_GAUSS, false>(scale, norm, x, mu);
-    return unit ? pdf_t<CBN_FAMILY_LOGISTIC, true>(scale, norm, x, mu) : pdf_t<CBN_FAMILY_LOGISTIC, false>(scale, norm, x, mu);
+__device__ __forceinline__ int mode_of(int family, bool unit) {
+    return (family == CBN_FAMILY_GAUSS ? 0 : 2) + (unit ? 0 : 1);
 }
 
-// fx[j] += pdf(S[j]; mu) for the chunk's columns (S, scale, norm wave-uniform)
-template <int NC, int FAM, bool UNIT>
-__device__ __forceinline__ void add_row_t(float (&fx)[NC], const float* __restrict__ S, int ncol, float sc, float nm,
-                                          float mu) {
-#pragma unroll
-    for (int j = 0; j < NC; ++j)
-        if (j < ncol) fx[j] += pdf_t<FAM, UNIT>(sc, nm, S[j], mu);
-}
-
-template <int NC>
-__device__ __forceinline__ void add_row(int mode, float (&fx)[NC], const float* __restrict__ S, int ncol, float sc,
-                                        float nm, float mu) {
+__device__ __forceinline__ float pdf_eval(int mode, float scale, float inv_scale, float norm, float x, float mu) {
     switch (mode) {
-        case 0: add_row_t<NC, CBN_FAMILY_GAUSS, true>(fx, S, ncol, sc, nm, mu); break;
-        case 1: add_row_t<NC, CBN_FAMILY_GAUSS, false>(fx, S, ncol, sc, nm, mu); break;
-        case 2: add_row_t<NC, CBN_FAMILY_LOGISTIC, true>(fx, S, ncol, sc, nm, mu); break;
-        default: add_row_t<NC, CBN_FAMILY_LOGISTIC, false>(fx, S, ncol, sc, nm, mu); break;
+        case 0: return pdf_t<0>(scale, inv_scale, norm, x, mu);
+        case 1: return pdf_t<1>(scale, inv_scale, norm, x, mu);
+        case 2: return pdf_t<2>(scale, inv_scale, norm, x, mu);
+        default: return pdf_t<3>(scale, inv_scale, norm, x, mu);
     }
 }
 
-// Query kernel.  Wave task t -> column chunk l = t / QW (uniform) and the 64
-// consecutive queries (t % QW) * 64 + lane; every lane keeps its NC outputs'
-// running product in registers.  Writes the UNnormalised rows and one max
-// word per block (the global-max division of bayesian_network.py:296 runs
-// after, in k_scale, possibly after a cross-rank all-reduce of the words).
-template <int NC, int HMAX>
-__global__ void __launch_bounds__(kThreads)
-k_param_query(const float* __restrict__ img, int nf, PEv ev, long long Q, int N, int L, long long QW, int n_words,
-              unsigned* __restrict__ max_out, float* __restrict__ out) {
+// fx[j] += pdf(S[j]; mu) over the chunk (S, scale, norm wave-uniform; S rows
+// are padded to a multiple of kColPad, so no column predicates)
+template <int NC, int MODE>
+__device__ __forceinline__ void add_row_t(float (&fx)[NC], const float* __restrict__ S, float sc, float isc,
+                                          float nm, float mu) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) fx[j] += pdf_t<MODE>(sc, isc, nm, S[j], mu);
+}
+
+// acc[j] *= pdf(S[j]; mu): the M == 1 factor (a mean over size-1 axes is the pdf itself)
+template <int NC, int MODE>
+__device__ __forceinline__ void mul_row_t(float (&acc)[NC], const float* __restrict__ S, float sc, float isc,
+                                          float nm, float mu) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * pdf_t<MODE>(sc, isc, nm, S[j], mu);
+}
+
+template <int NC, int MODE>
+__device__ __forceinline__ void add_row(int mode, float (&fx)[NC], const float* __restrict__ S, float sc, float isc,
+                                        float nm, float mu) {
+    if (MODE < 4) {
+        add_row_t<NC, MODE < 4 ? MODE : 0>(fx, S, sc, isc, nm, mu);
+    } else {
+        switch (mode) {
+            case 0: add_row_t<NC, 0>(fx, S, sc, isc, nm, mu); break;
+            case 1: add_row_t<NC, 1>(fx, S, sc, isc, nm, mu); break;
+            case 2: add_row_t<NC, 2>(fx, S, sc, isc, nm, mu); break;
+            default: add_row_t<NC, 3>(fx, S, sc, isc, nm, mu); break;
+        }
+    }
+}
+
+// Column of one model input, resolved once per block into LDS: element
+// q of the input is p[q * stride] (stride 0: a constant / unused input reading
+// the image's {0, 1} cell).
+struct alignas(16) InCol {
+    const float* p;
+    long long stride;
+};
+
+// Evidence inputs of a factor (its kMaxP InCol entries): independent LDS reads
+// and vector loads, issued back to back; nothing waits on them until the
+// factor is evaluated.  Free inputs are overwritten per combo.
+__device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long long qs, float (&z)[kMaxP]) {
+#pragma unroll
+    for (int i = 0; i < kMaxP; ++i) {
+        const InCol c = cols[i];
+        z[i] = gload(c.p, qs * c.stride);
+    }
+}
+
+// Query kernel.  Wave task t -> column chunk l = t / QW and the 64
+// consecutive queries (t % QW) * 64 + lane (t, l, the chunk and every image
+// read wave-uniform: scalar loads into SGPRs); every lane keeps its NC
+// outputs' running product in registers and prefetches the next factor's
+// evidence while it evaluates the current one.  MODE: the density family of
+// every query factor (0..3, see pdf_t) or 4 = per-factor switch.  Writes the
+// UNnormalised rows and one max word per block (the global-max division of
+// bayesian_network.py:296 runs after, in k_scale, possibly after a cross-rank
+// all-reduce of the words).
+template <int NC, int HMAX, int MODE>
+__global__ void __launch_bounds__(kQThreads)
+k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
+              int n_words, unsigned* __restrict__ max_out, float* __restrict__ out) {
     const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);
-    extern __shared__ float deep_smem[];  // sized only for models with >= 2 hidden layers
-    float* deep = deep_smem + threadIdx.x;
+    // dynamic LDS: [nf x kMaxP InCol] [deep-model scratch, models with >= 2 hidden layers]
+    extern __shared__ __attribute__((aligned(16))) float4 smem_q[];
+    InCol* incol = reinterpret_cast<InCol*>(smem_q);
+    float* deep = reinterpret_cast<float*>(incol + nf * kMaxP) + threadIdx.x;
+    const float* cst = img + cst_off;
+    for (int e = threadIdx.x; e < nf * kMaxP; e += blockDim.x) {
+        const int sl = rec[e / kMaxP].in_slot[e % kMaxP];
+        InCol c;
+        c.p = sl >= 0 ? ev.p[sl] : (sl == CBN_INPUT_ONE ? cst + 1 : cst);
+        c.stride = sl >= 0 ? 1 : 0;
+        incol[e] = c;
+    }
+    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
-    const int wpb = kThreads / kWave;
-    const long long tasks = QW * L;
+    const int wpb = kQThreads / kWave;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int tasks = QW * L;
     float lmax = 0.f;
-    for (long long t = (long long)blockIdx.x * wpb + threadIdx.x / kWave; t < tasks; t += (long long)gridDim.x * wpb) {
-        const int l = (int)(t / QW);
-        const long long q = (t - (long long)l * QW) * kWave + lane;
+    for (int t = blockIdx.x * wpb + wid; t < tasks; t += gridDim.x * wpb) {
+        const int l = t / QW;
+        const long long q = (long long)(t - l * QW) * kWave + lane;
         const bool valid = q < Q;
         const long long qs = valid ? q : Q - 1;
         const int col0 = l * NC;
-        const int ncol = min(NC, N - col0);  // wave-uniform
+        const int ncol = min(NC, N - col0);
         float acc[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        float z[kMaxP];
+        load_inputs(incol, qs, z);
         for (int f = 0; f < nf; ++f) {
             const PRec& r = rec[f];
+            float zn[kMaxP];
+            load_inputs(incol + (f + 1 < nf ? f + 1 : f) * kMaxP, qs, zn);  // in flight during this factor
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
                 const float* c = img + r.c_off + col0;
 #pragma unroll
-                for (int j = 0; j < NC; ++j)
-                    if (j < ncol) acc[j] = acc[j] * c[j];
-                continue;
-            }
-            const int n_in = r.m.width[0];
-            float z[kMaxP];
+                for (int j = 0; j < NC; ++j) acc[j] = acc[j] * c[j];
+            } else {
+                const float* W = img + r.w_off;
+                const float* S = img + r.s_off + col0;
+                const int mode = mode_of(r.family, r.unit != 0);
+                const float sc = r.scale, isc = r.inv_scale, nm = r.norm;
+                if (HMAX == 0 && MODE < 4 && r.M == 1) {  // linear model, every parent observed
+                    mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, S, sc, isc, nm, model_mu<0>(r.m, W, z, deep));
 #pragma unroll
-            for (int i = 0; i < kMaxP; ++i) {
-                z[i] = 0.f;
-                if (i < n_in) {
-                    const int sl = r.in_slot[i];
-                    if (sl >= 0) z[i] = gload(ev.p[sl], qs);
-                    else if (sl == CBN_INPUT_ONE) z[i] = 1.f;
+                    for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
+                    continue;
                 }
-            }
-            const float* W = img + r.w_off;
-            const float* S = img + r.s_off + col0;
-            const int mode = (r.family == CBN_FAMILY_GAUSS ? 0 : 2) + (r.unit ? 0 : 1);
-            const float sc = r.scale, nm = r.norm;
-            float fx[NC];
+                float fx[NC];
 #pragma unroll
-            for (int j = 0; j < NC; ++j) fx[j] = 0.f;
-            const float* FS = img + r.fs_off;
-            // M == 1 (every parent observed): one pass, x = pdf (a mean over size-1 axes)
-            for (int c = 0; c < r.M; ++c) {
-                int cc = c;  // meshgrid 'ij' order: last free input fastest (node.py:335-375)
+                for (int j = 0; j < NC; ++j) fx[j] = 0.f;
+                const float* FS = img + r.fs_off;
+                // M == 1 (every parent observed): one pass, x = pdf (a mean over size-1 axes)
+                const int fm = r.free_mask;
+                for (int c = 0; c < r.M; ++c) {
+                    if (fm) {
+                        int cc = c;  // meshgrid 'ij' order: last free input fastest (node.py:335-375)
 #pragma unroll
-                for (int i = kMaxP - 1; i >= 0; --i) {
-                    if (i < n_in && r.in_slot[i] == CBN_INPUT_FREE) {
-                        const int qd = cc / N;
-                        z[i] = FS[i * N + (cc - qd * N)];
-                        cc = qd;
+                        for (int i = kMaxP - 1; i >= 0; --i) {
+                            if (fm & (1 << i)) {
+                                const int qd = cc / N;
+                                z[i] = FS[i * N + (cc - qd * N)];
+                                cc = qd;
+                            }
+                        }
                     }
+                    add_row<NC, MODE>(mode, fx, S, sc, isc, nm, model_mu<HMAX, kQThreads>(r.m, W, z, deep));
                 }
-                add_row<NC>(mode, fx, S, ncol, sc, nm, model_mu<HMAX>(r.m, W, z, deep));
-            }
-            if (r.M > 1) {
-                const float Mf = (float)r.M;
+                if (r.M > 1) {
+                    const float Mf = (float)r.M;
 #pragma unroll
-                for (int j = 0; j < NC; ++j) fx[j] = fx[j] / Mf;  // torch.mean = sum / count
+                    for (int j = 0; j < NC; ++j) fx[j] = fx[j] / Mf;  // torch.mean = sum / count
+                }
+#pragma unroll
+                for (int j = 0; j < NC; ++j) acc[j] = acc[j] * fx[j];
             }
 #pragma unroll
-            for (int j = 0; j < NC; ++j) acc[j] = acc[j] * fx[j];
+            for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
         }
         if (valid) {
             float* o = out + q * N + col0;
@@ -319,7 +414,7 @@ k_param_query(const float* __restrict__ img, int nf, PEv ev, long long Q, int N,
         }
     }
     // block max -> one word per block (non-negative floats: uint order == float order)
-    __shared__ unsigned wm[kThreads / kWave];
+    __shared__ unsigned wm[kQThreads / kWave];
     const unsigned wmx = wave_max_u(__float_as_uint(lmax));
     if (lane == 0) wm[threadIdx.x / kWave] = wmx;
     __syncthreads();
@@ -329,7 +424,7 @@ k_param_query(const float* __restrict__ img, int nf, PEv ev, long long Q, int N,
         max_out[blockIdx.x] = m;
     }
     if (blockIdx.x == 0)  // words of blocks this launch does not have
-        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += kThreads) max_out[i] = 0u;
+        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += kQThreads) max_out[i] = 0u;
 }
 
 // Query-independent factors, once per plan: SHARED x[j] = mean_c pdf(s_j;
@@ -364,7 +459,7 @@ k_param_const(float* __restrict__ img, const int* __restrict__ which, int N) {
                     cc = qd;
                 }
             }
-            s += pdf_eval(r.family, unit, r.scale, r.norm, S[js], model_mu<HMAX>(r.m, W, z, deep));
+            s += pdf_eval(mode_of(r.family, unit), r.scale, r.inv_scale, r.norm, S[js], model_mu<HMAX>(r.m, W, z, deep));
         }
         if (j < N) C[j] = r.kind == CBN_FACTOR_SCALAR ? s : s / (float)r.M;
     }
@@ -401,8 +496,10 @@ k_param_eval(MDesc m, int family, int unit, float scale, float norm, const float
             for (int i = 0; i < kMaxP; ++i) z[i] = i < n_in ? (query ? query[r * n_in + i] : 1.f) : 0.f;
             mu = model_mu<HMAX>(m, W, z, deep);
         }
+        const int mode = mode_of(family, unit != 0);
+        const float inv_scale = 1.f / scale;
         for (int v = 0; v < n_pts; ++v)
-            out[r * n_pts + v] = pdf_eval(family, unit != 0, scale, norm, pts[r * n_pts + v], mu);
+            out[r * n_pts + v] = pdf_eval(mode, scale, inv_scale, norm, pts[r * n_pts + v], mu);
     }
 }
 
@@ -438,14 +535,18 @@ int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const 
 }
 
 // LDS scratch of the deep-model path (>= 2 hidden layers): 2 x HMAX floats per thread
-size_t deep_bytes(const MDesc& m, int hmax) {
-    return m.n_layers > 2 ? (size_t)2 * hmax * kThreads * sizeof(float) : 0;
+size_t deep_bytes(const MDesc& m, int hmax, int threads = kThreads) {
+    return m.n_layers > 2 ? (size_t)2 * hmax * threads * sizeof(float) : 0;
 }
 
+// dynamic LDS beyond the 64 KiB default (the kernels' static LDS is < 256 B);
+// a refusal must not linger as the thread's sticky last error
+constexpr int kDynLdsMax = kLdsBudget - 256;
 template <typename K>
 void allow_deep(K* k) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * 32 * kThreads * (int)sizeof(float));
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, kDynLdsMax) !=
+        hipSuccess)
+        (void)hipGetLastError();
 }
 
 template <int HMAX>
@@ -468,7 +569,10 @@ struct ParamPlan {
     int nc = 16;     // output columns per lane
     int L = 1;       // column chunks per query
     int hmax = 0;    // 0 / 16 / 32
-    size_t deep = 0; // dynamic LDS of the deep-model path
+    int mode = 4;    // density family of every query factor (0..3) or 4: mixed
+    int cst_off = 0; // image offset of the {0, 1} cell read by constant inputs
+    size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
+    size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
     float* d_image = nullptr;
     int* d_which = nullptr;
@@ -477,22 +581,32 @@ struct ParamPlan {
 }  // namespace cbn
 
 namespace {
-template <int NC, int HMAX>
-void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
+template <int NC, int HMAX, int MODE>
+void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
                     unsigned* words, float* out, hipStream_t s) {
-    allow_deep(&k_param_query<NC, HMAX>);
-    hipLaunchKernelGGL((k_param_query<NC, HMAX>), dim3(grid), dim3(kThreads), pp->deep, s, pp->d_image, pp->nf, ev, Q,
-                       pp->N, pp->L, QW, pp->max_slots, words, out);
+    allow_deep(&k_param_query<NC, HMAX, MODE>);
+    const size_t lds = (size_t)pp->nf * kMaxP * sizeof(InCol) + pp->deep;
+    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
+                       pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out);
 }
 
+// Instantiated (HMAX, MODE) pairs: linear models (HMAX 0) of either family,
+// MLPs with the logistic density (NeuralNetwork); anything else runs the
+// per-factor switch at NC = 16, HMAX = 32 (plan_create picks nc/L for it).
+bool specialised(int hmax, int mode) { return mode < 4 && (hmax == 0 || mode >= 2); }
+
+// MLP (NeuralNetwork, logistic density) kernels for one column chunk
 template <int NC>
-void launch_query_nc(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
-                     unsigned* words, float* out, hipStream_t s) {
-    switch (pp->hmax) {
-        case 0: launch_query_t<NC, 0>(pp, grid, ev, Q, QW, words, out, s); break;
-        case 16: launch_query_t<NC, 16>(pp, grid, ev, Q, QW, words, out, s); break;
-        default: launch_query_t<NC, 32>(pp, grid, ev, Q, QW, words, out, s); break;
+void launch_query_mlp(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
+                      unsigned* words, float* out, hipStream_t s) {
+#define CBN_Q(H, M) launch_query_t<NC, H, M>(pp, grid, ev, Q, QW, L, words, out, s)
+    switch (pp->hmax * 8 + pp->mode) {
+        case 16 * 8 + 2: CBN_Q(16, 2); break;
+        case 16 * 8 + 3: CBN_Q(16, 3); break;
+        case 32 * 8 + 2: CBN_Q(32, 2); break;
+        default: CBN_Q(32, 3); break;
     }
+#undef CBN_Q
 }
 }  // namespace
 
@@ -519,15 +633,33 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
         ev.p[i] = evidence[i];
     }
     const long long QW = (n_queries + kWave - 1) / kWave;
-    const long long waves = QW * pp->L;
-    long long grid = (waves + kThreads / kWave - 1) / (kThreads / kWave);
+    // column chunk: linear models (mu costs a few FMAs) take 8 columns per lane
+    // (<= 64 VGPRs: 8 waves per SIMD); MLPs keep whole rows up to 32 columns
+    // (every extra chunk re-evaluates the network)
+    int nc = pp->nc;
+    if (pp->hmax == 0 && specialised(pp->hmax, pp->mode)) nc = 8;
+    const int L = (pp->N + nc - 1) / nc;
+    const long long waves = QW * L;
+    if (waves >= (1LL << 31)) return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
+    long long grid = (waves + kQThreads / kWave - 1) / (kQThreads / kWave);
     grid = std::max(1LL, std::min(grid, (long long)pp->max_slots));
     const bool raw = (flags & CBN_RUN_RAW) != 0;
     unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
-    switch (pp->nc) {
-        case 8: launch_query_nc<8>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
-        case 16: launch_query_nc<16>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
-        default: launch_query_nc<32>(pp, (unsigned)grid, ev, n_queries, QW, words, out, s); break;
+    if (!specialised(pp->hmax, pp->mode)) {
+        launch_query_t<16, 32, 4>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s);
+    } else if (pp->hmax == 0) {  // linear models: 8-column chunks
+        switch (pp->mode) {
+            case 0: launch_query_t<8, 0, 0>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            case 1: launch_query_t<8, 0, 1>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            case 2: launch_query_t<8, 0, 2>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            default: launch_query_t<8, 0, 3>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+        }
+    } else {
+        switch (nc) {
+            case 8: launch_query_mlp<8>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            case 16: launch_query_mlp<16>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            default: launch_query_mlp<32>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+        }
     }
     PHIP_TRY(hipGetLastError());
     if (raw) return CBN_OK;
@@ -544,7 +676,8 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     const int N = n_samples;
     std::vector<PRec> recs(n_factors);
     std::vector<int> consts;
-    long long off = (long long)n_factors * kRecFloats;
+    const long long cst_off = (long long)n_factors * kRecFloats;  // {0, 1}: constant model inputs
+    long long off = cst_off + 4;
     int ns = 0, hmax = 0;
     for (int f = 0; f < n_factors; ++f) {
         const cbn_param_factor& h = factors[f];
@@ -559,6 +692,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         if (!h.node_samples) return set_err(CBN_E_ARG, "factor %d: null node samples", f);
         int n_obs = 0, n_free = 0;
         long long M = 1;
+        for (int i = 0; i < kMaxP; ++i) r.in_slot[i] = kInputNone;
         for (int i = 0; i < r.m.width[0]; ++i) {
             const int sl = h.input_slot[i];
             if (sl >= 0) {
@@ -567,6 +701,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
                 ++n_obs;
             } else if (sl == CBN_INPUT_FREE) {
                 ++n_free;
+                r.free_mask |= 1 << i;
                 M *= N;
                 if (M >= (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: too many free-parent combos", f);
             } else if (sl != CBN_INPUT_ONE) {
@@ -581,20 +716,22 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         r.kind = h.kind;
         r.family = h.model.family;
         r.scale = h.model.scale;
+        r.inv_scale = 1.f / h.model.scale;
         r.norm = h.model.norm;
         r.unit = h.model.scale == 1.f ? 1 : 0;
         r.M = (int)M;
         r.w_off = (int)off;
         off += (nw + 3) & ~3LL;
+        const long long row = (N + kColPad - 1) / kColPad * kColPad;  // padded: chunk reads never leave the row
         r.s_off = (int)off;
-        off += (N + 3) & ~3;
+        off += row;
         if (n_free > 0) {
             r.fs_off = (int)off;
             off += ((long long)r.m.width[0] * N + 3) & ~3LL;
         }
         if (h.kind != CBN_FACTOR_QUERY) {
             r.c_off = (int)off;
-            off += (N + 3) & ~3;
+            off += row;
             consts.push_back(f);
         }
         if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "parametric plan image too large");
@@ -604,8 +741,23 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     pp->N = N;
     pp->ns = ns;
     pp->hmax = hmax;
-    for (const PRec& r : recs) pp->deep = std::max(pp->deep, deep_bytes(r.m, hmax));
+    for (const PRec& r : recs) {
+        pp->deep = std::max(pp->deep, deep_bytes(r.m, hmax, kQThreads));
+        pp->deep_const = std::max(pp->deep_const, deep_bytes(r.m, hmax));
+    }
+    pp->mode = -1;
+    for (const PRec& r : recs) {
+        if (r.kind != CBN_FACTOR_QUERY) continue;
+        const int m = (r.family == CBN_FAMILY_GAUSS ? 0 : 2) + (r.unit ? 0 : 1);
+        pp->mode = pp->mode < 0 || pp->mode == m ? m : 4;
+    }
+    if (pp->mode < 0) pp->mode = 0;  // no query factor
     pp->image_floats = (int)off;
+    pp->cst_off = (int)cst_off;
+    if ((size_t)n_factors * kMaxP * sizeof(InCol) + pp->deep > (size_t)kDynLdsMax) {
+        delete pp;
+        return set_err(CBN_E_LIMIT, "parametric plan: %d factors need more LDS than a CU has", n_factors);
+    }
     // column chunk per lane: whole rows when they fit (the model runs once
     // per query and factor), else 32-column chunks
     int nc = 32;
@@ -614,6 +766,10 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     if (const char* e = getenv("CBN_PARAM_NC")) {
         const int v = atoi(e);
         if (v == 8 || v == 16 || v == 32) nc = v;
+    }
+    if (!specialised(hmax, pp->mode)) {
+        nc = 16;  // the one generic instantiation
+        if (hmax > 0) pp->hmax = 32;
     }
     pp->nc = nc;
     pp->L = (N + nc - 1) / nc;
@@ -629,6 +785,8 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     ok = ok && hipMemset(pp->d_image, 0, sizeof(float) * (size_t)off) == hipSuccess;
     ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
     ok = ok && hipMemcpy(pp->d_image, recs.data(), sizeof(PRec) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
+    const float cst[4] = {0.f, 1.f, 0.f, 0.f};
+    ok = ok && hipMemcpy(pp->d_image + cst_off, cst, sizeof(cst), hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && (consts.empty() ||
                 hipMemcpy(pp->d_which, consts.data(), sizeof(int) * consts.size(), hipMemcpyHostToDevice) == hipSuccess);
     for (int f = 0; ok && f < n_factors; ++f) {
@@ -645,9 +803,9 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     ok = ok && hipDeviceSynchronize() == hipSuccess;
     if (ok && !consts.empty()) {
         switch (hmax) {
-            case 0: launch_const_t<0>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
-            case 16: launch_const_t<16>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
-            default: launch_const_t<32>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep, nullptr); break;
+            case 0: launch_const_t<0>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
+            case 16: launch_const_t<16>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
+            default: launch_const_t<32>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
         }
         ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     }

@@ -239,3 +239,63 @@ def test_config3_full_size_properties(est, model, gpu):
     ref, _ = ora.infer(cols[-1], {k: v[sub] for k, v in ev.items()}, 16)
     scale = p[sub].max() / ref.max()
     np.testing.assert_allclose(p[sub], ref * scale, rtol=2e-5, atol=1e-7)
+
+
+def _set_linear(est, W, b, log_scale, gpu):
+    est.linear_model.weight.data = torch.tensor(W, dtype=torch.float32, device=gpu)
+    est.linear_model.bias.data = torch.tensor(b, dtype=torch.float32, device=gpu)
+    getattr(est, "log_sigma", None) is not None and setattr(est.log_sigma, "data",
+                                                            torch.tensor(log_scale, device=gpu))
+    getattr(est, "log_scale", None) is not None and setattr(est.log_scale, "data",
+                                                            torch.tensor(log_scale, device=gpu))
+    est._invalidate()
+
+
+def test_density_accuracy_full_range(gpu):
+    """The kernels' exp (split x*log2e + v_exp_f32) and Newton-refined divisions
+    vs float64 over the whole fp32 range of the two densities: <= 4 ulp where
+    the float64 value is a normal fp32; subnormal results (< 2^-126) flush to 0
+    (documented deviation: the reference keeps the subnormal); overflow gives
+    the reference's NaN (logistic: inf / inf)."""
+    from continuousbayesiannetwork_amd.parameter_learning import LogisticRegression
+
+    tiny = np.float32(2.0 ** -126)
+    x = np.linspace(-14.6, 14.6, 200001, dtype=np.float32)
+    q = np.zeros((x.size, 1, 1), np.float32)
+    lr = LinearRegression(param_config("linear_regression", n_epochs=1), device=gpu)
+    lr.fit(torch.tensor(x[:100], device=gpu), torch.tensor(x[None, :100], device=gpu))
+    for ls in (0.0, -0.7, 1.3):  # sigma = 1 (unit path) and scaled
+        _set_linear(lr, [[0.0]], [0.0], ls, gpu)
+        got = lr.get_prob(torch.tensor(x[:, None], device=gpu), torch.tensor(q, device=gpu)).cpu().numpy()[:, 0]
+        # sigma / norm exactly as the estimator computes them (torch CPU float32,
+        # linear_regression.py:91-95): d pdf / pdf = t^2 per unit relative change of t
+        sig_t = torch.exp(torch.tensor(ls, dtype=torch.float32))
+        sig = np.float32(sig_t.item())
+        norm = np.float32((1 / (sig_t * torch.sqrt(torch.tensor(2 * torch.pi)))).item())
+        t = (x / sig).astype(np.float32)
+        ideal = (np.float64(norm) * np.exp(np.float64(np.float32(-0.5) * (t * t)))).astype(np.float32)
+        normal = ideal >= tiny
+        ulp = np.abs(got[normal].astype(np.float64) - ideal[normal]) / np.spacing(ideal[normal])
+        assert ulp.max() <= 4, (ls, ulp.max())
+        assert np.all((got[~normal] == 0) | (np.abs(got[~normal] - ideal[~normal]) <= tiny))
+    lg = LogisticRegression(param_config("logistic_regression", n_epochs=1), device=gpu)
+    lg.fit(torch.tensor(np.zeros(100, np.float32), device=gpu), torch.tensor(x[None, :100], device=gpu))
+    d = np.linspace(-95.0, 95.0, 200001, dtype=np.float32)
+    for ls in (0.0, 0.4):
+        _set_linear(lg, [[0.0]], [0.0], ls, gpu)
+        got = lg.get_prob(torch.tensor(d[:, None], device=gpu), torch.tensor(q, device=gpu)).cpu().numpy()[:, 0]
+        s = np.float32(torch.exp(torch.tensor(ls, dtype=torch.float32)).item())
+        dd = (d / s).astype(np.float32)
+        with np.errstate(over="ignore", invalid="ignore"):
+            e32 = np.exp(-dd)  # the reference's float32 path decides inf / NaN
+            u = (np.float32(1) + e32).astype(np.float32)
+            ref32 = (e32 / (s * u * u)).astype(np.float32)
+            e = np.exp(-np.float64(dd))
+            ideal = (e / (np.float64(s) * (1 + e) ** 2)).astype(np.float32)
+        nan = np.isnan(ref32)
+        np.testing.assert_array_equal(np.isnan(got), nan)
+        zero = ~nan & (ref32 == 0)
+        assert np.all(got[zero] == 0)
+        normal = ~nan & ~zero & (ideal >= tiny)  # zero: the reference's (1 + e)^2 overflowed
+        ulp = np.abs(got[normal].astype(np.float64) - ideal[normal]) / np.spacing(ideal[normal])
+        assert ulp.max() <= 4, (ls, ulp.max())
