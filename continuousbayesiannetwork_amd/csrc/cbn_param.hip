@@ -74,8 +74,15 @@ struct alignas(16) PRec {
 static_assert(sizeof(PRec) == 128, "PRec layout");
 constexpr int kRecFloats = sizeof(PRec) / 4;
 
+// Kernel-argument pointer table (3 KiB of the 4 KiB kernarg space).  Table
+// mode: p[f * kTabIn + i] = column of input i of factor f (evidence, or a
+// dummy column -- the output buffer, >= Q floats -- for inputs that are not
+// evidence: their loads are ignored), read with scalar loads into SGPRs.
+// Slot mode (plans beyond the table): p[slot] = evidence column of the slot.
+constexpr int kTabIn = 4;
+constexpr int kTabCols = 384;  // 96 factors x 4 inputs
 struct PEv {
-    const float* p[CBN_MAX_EVIDENCE];
+    const float* p[kTabCols];
 };
 
 typedef const __attribute__((address_space(1))) float gfloat_t;
@@ -301,6 +308,13 @@ __device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long
     }
 }
 
+__device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, long long qs, float (&z)[kMaxP]) {
+#pragma unroll
+    for (int i = 0; i < kTabIn; ++i) z[i] = gload(ev.p[f * kTabIn + i], qs);
+#pragma unroll
+    for (int i = kTabIn; i < kMaxP; ++i) z[i] = 0.f;
+}
+
 // Query kernel.  Wave task t -> column chunk l = t / QW and the 64
 // consecutive queries (t % QW) * 64 + lane (t, l, the chunk and every image
 // read wave-uniform: scalar loads into SGPRs); every lane keeps its NC
@@ -310,7 +324,7 @@ __device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long
 // UNnormalised rows and one max word per block (the global-max division of
 // bayesian_network.py:296 runs after, in k_scale, possibly after a cross-rank
 // all-reduce of the words).
-template <int NC, int HMAX, int MODE>
+template <int NC, int HMAX, int MODE, bool TAB>
 __global__ void __launch_bounds__(kQThreads)
 k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
               int n_words, unsigned* __restrict__ max_out, float* __restrict__ out) {
@@ -318,16 +332,18 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
     // dynamic LDS: [nf x kMaxP InCol] [deep-model scratch, models with >= 2 hidden layers]
     extern __shared__ __attribute__((aligned(16))) float4 smem_q[];
     InCol* incol = reinterpret_cast<InCol*>(smem_q);
-    float* deep = reinterpret_cast<float*>(incol + nf * kMaxP) + threadIdx.x;
-    const float* cst = img + cst_off;
-    for (int e = threadIdx.x; e < nf * kMaxP; e += blockDim.x) {
-        const int sl = rec[e / kMaxP].in_slot[e % kMaxP];
-        InCol c;
-        c.p = sl >= 0 ? ev.p[sl] : (sl == CBN_INPUT_ONE ? cst + 1 : cst);
-        c.stride = sl >= 0 ? 1 : 0;
-        incol[e] = c;
+    float* deep = reinterpret_cast<float*>(incol + (TAB ? 0 : nf * kMaxP)) + threadIdx.x;
+    if (!TAB) {
+        const float* cst = img + cst_off;
+        for (int e = threadIdx.x; e < nf * kMaxP; e += blockDim.x) {
+            const int sl = rec[e / kMaxP].in_slot[e % kMaxP];
+            InCol c;
+            c.p = sl >= 0 ? ev.p[sl] : (sl == CBN_INPUT_ONE ? cst + 1 : cst);
+            c.stride = sl >= 0 ? 1 : 0;
+            incol[e] = c;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int wpb = kQThreads / kWave;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -344,11 +360,14 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
-        load_inputs(incol, qs, z);
+        if (TAB) load_inputs_tab(ev, 0, qs, z);
+        else load_inputs(incol, qs, z);
         for (int f = 0; f < nf; ++f) {
             const PRec& r = rec[f];
             float zn[kMaxP];
-            load_inputs(incol + (f + 1 < nf ? f + 1 : f) * kMaxP, qs, zn);  // in flight during this factor
+            const int fn = f + 1 < nf ? f + 1 : f;  // next factor's evidence in flight during this one
+            if (TAB) load_inputs_tab(ev, fn, qs, zn);
+            else load_inputs(incol + fn * kMaxP, qs, zn);
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
                 const float* c = img + r.c_off + col0;
 #pragma unroll
@@ -571,6 +590,8 @@ struct ParamPlan {
     int hmax = 0;    // 0 / 16 / 32
     int mode = 4;    // density family of every query factor (0..3) or 4: mixed
     int cst_off = 0; // image offset of the {0, 1} cell read by constant inputs
+    bool tab_ok = false;  // <= kTabIn inputs per factor and nf * kTabIn <= kTabCols: kernarg column table
+    std::vector<int> in_slot;  // [nf][kTabIn] host copy (table mode)
     size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
     size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
@@ -581,12 +602,12 @@ struct ParamPlan {
 }  // namespace cbn
 
 namespace {
-template <int NC, int HMAX, int MODE>
+template <int NC, int HMAX, int MODE, bool TAB = (MODE < 4)>
 void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
                     unsigned* words, float* out, hipStream_t s) {
-    allow_deep(&k_param_query<NC, HMAX, MODE>);
-    const size_t lds = (size_t)pp->nf * kMaxP * sizeof(InCol) + pp->deep;
-    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
+    allow_deep(&k_param_query<NC, HMAX, MODE, TAB>);
+    const size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
+    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
                        pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out);
 }
 
@@ -628,9 +649,15 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     if (!pp->d_image || !plan->d_sync) return set_err(CBN_E_ARG, "plan has no device buffers");
     PEv ev;
     memset(&ev, 0, sizeof(ev));
-    for (int i = 0; i < n_evidence; ++i) {
+    for (int i = 0; i < n_evidence; ++i)
         if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
-        ev.p[i] = evidence[i];
+    if (specialised(pp->hmax, pp->mode)) {  // table mode: one pointer per (factor, input)
+        for (size_t e = 0; e < pp->in_slot.size(); ++e) {
+            const int sl = pp->in_slot[e];
+            ev.p[e] = sl >= 0 ? evidence[sl] : out;  // dummy column (>= Q floats), value unused
+        }
+    } else {
+        for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
     }
     const long long QW = (n_queries + kWave - 1) / kWave;
     // column chunk: linear models (mu costs a few FMAs) take 8 columns per lane
@@ -754,6 +781,16 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     if (pp->mode < 0) pp->mode = 0;  // no query factor
     pp->image_floats = (int)off;
     pp->cst_off = (int)cst_off;
+    pp->tab_ok = (long long)n_factors * kTabIn <= kTabCols;
+    for (const PRec& r : recs)
+        for (int i = kTabIn; i < kMaxP; ++i) pp->tab_ok = pp->tab_ok && r.in_slot[i] == kInputNone;
+    if (pp->tab_ok) {
+        pp->in_slot.resize((size_t)n_factors * kTabIn);
+        for (int f = 0; f < n_factors; ++f)
+            for (int i = 0; i < kTabIn; ++i) pp->in_slot[f * kTabIn + i] = recs[f].in_slot[i];
+    } else {
+        pp->mode = 4;  // the slot-mode (LDS column table) kernel is the generic one
+    }
     if ((size_t)n_factors * kMaxP * sizeof(InCol) + pp->deep > (size_t)kDynLdsMax) {
         delete pp;
         return set_err(CBN_E_LIMIT, "parametric plan: %d factors need more LDS than a CU has", n_factors);
