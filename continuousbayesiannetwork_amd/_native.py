@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so"
 
 ABI_VERSION = 2
 CBN_MAX_PARENTS = 8
-CBN_MAX_EVIDENCE = 64
+CBN_MAX_EVIDENCE = 256
 CBN_FACTOR_SCALAR = 0
 CBN_FACTOR_SHARED = 1
 CBN_FACTOR_QUERY = 2

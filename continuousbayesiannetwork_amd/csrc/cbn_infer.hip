@@ -1062,8 +1062,21 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     const int N = n_samples;
     const int vec = (N % 4 == 0) ? 4 : 1;
     const int L = N / vec;
-    const int RS = vec == 4 ? N + 4 : N;  // +16 B per row: consecutive rows start 4 banks apart
     if (L > kQueryThreads) return set_err(CBN_E_LIMIT, "N_max %d too large for one block row", N);
+    // Table rows: in LDS, +16 B per row so consecutive rows start 4 banks apart;
+    // an image that cannot fit LDS is read from L2/HBM, where the pad would make
+    // every row straddle one more cache line: unpadded rows, 128-B aligned tables.
+    long long total_rows = 0;
+    for (int f = 0; f < n_factors; ++f) {
+        long long rows = 1;
+        for (int p = 0; p < factors[f].n_parents && p < kMaxP; ++p)
+            if (factors[f].parent_ev_slot[p] >= 0 && factors[f].parent_card[p] > 0)
+                rows = std::min(rows * factors[f].parent_card[p], 1LL << 40);
+        total_rows += rows;
+    }
+    const bool global_tables = vec == 4 && total_rows * (N + 4) * 4 > (long long)kLdsBudget;
+    const int RS = vec == 4 && !global_tables ? N + 4 : N;
+    const long long talign = global_tables ? 32 : 4;
     std::vector<DevFactor> fac(n_factors);
     std::vector<const float*> slot_dom(CBN_MAX_EVIDENCE, nullptr);
     std::vector<int> slot_card(CBN_MAX_EVIDENCE, 0);
@@ -1123,7 +1136,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         const long long F_eff = h.kind == CBN_FACTOR_SCALAR ? N : F;
         d.wave_mode = F_eff >= kWave ? 1 : 0;
         d.table_off = (int)off;
-        off += (rows * RS + 3) & ~3LL;
+        off += (rows * RS + talign - 1) & ~(talign - 1);
     }
     for (int sl = 0; sl < ns; ++sl)
         if (!slot_dom[sl]) return set_err(CBN_E_ARG, "evidence slot %d is not used by any factor", sl);
@@ -1165,8 +1178,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         size_t ch = (avail - fixed) / per_q;
         return (int)std::min<size_t>(ch, 1024);
     };
-    int ch = chunk_for(kLdsBudget > img_bytes ? kLdsBudget - img_bytes : 0);
-    P->use_lds = ch >= 64;
+    int ch = global_tables ? 0 : chunk_for(kLdsBudget > img_bytes ? kLdsBudget - img_bytes : 0);
+    P->use_lds = ch >= 64;  // (a global-table layout stays in L2/HBM even if the unpadded image would fit)
     if (!P->use_lds) ch = chunk_for(kLdsBudget);
     if (ch < 1) {
         delete P;

@@ -15,7 +15,7 @@ namespace cbn {
 
 constexpr int kWave = 64;
 constexpr int kLdsBudget = 160 * 1024;
-constexpr int kFastPtrs = 256;  // fast table path: 64 factors x 4 observed parents
+constexpr int kFastPtrs = 416;  // fast table path: 104 factors x 4 observed parents (3.3 KiB of kernel arguments)
 
 // plan sync buffer (unsigned words): line 0 = timeout flag (word 2) and the
 // max/raw passes' max staging + arrival counter (words 4-5); from word

@@ -147,8 +147,25 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
         for (int i = 0; i < kMaxP; ++i)
             if (i < n_in) s = fmaf(W[i], z[i], s);
         return s + W[n_in];
+    } else if (HMAX == 1 || m.n_layers == 2) {
+        // one hidden layer (the reference's default, neural_network.py:37):
+        // stream over the hidden units -- mu = b2 + sum_o W2[o] act(W1[o] . z + b1[o])
+        // in o order, the same fma chain as the output layer's dot product, with
+        // only a handful of weights live at a time
+        const int H = m.width[1];
+        const float* B1 = W + H * n_in;
+        const float* W2 = B1 + H;
+        float mu = 0.f;
+        for (int o = 0; o < H; ++o) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < kMaxP; ++i)
+                if (i < n_in) s = fmaf(W[o * n_in + i], z[i], s);
+            mu = fmaf(W2[o], act1(m.act, s + B1[o]), mu);
+        }
+        return mu + W2[H];
     } else {
-        constexpr int H = HMAX > 0 ? HMAX : 1;
+        constexpr int H = HMAX > 1 ? HMAX : 1;
         float h[H];
         int win = m.width[1];
         const float* B = W + win * n_in;
@@ -522,11 +539,14 @@ k_param_eval(MDesc m, int family, int unit, float scale, float norm, const float
     }
 }
 
+// model kernel class: 0 linear, 1 one hidden layer (streamed), 32 deeper
+// (first hidden layer in registers, further ones in LDS)
 int hmax_for(const MDesc& m) {
     if (m.n_layers == 1) return 0;
+    if (m.n_layers == 2) return 1;
     int w = 0;
     for (int l = 1; l < m.n_layers; ++l) w = std::max(w, m.width[l]);
-    return w <= 16 ? 16 : 32;
+    return 32;
 }
 
 int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const char* what, int idx) {
@@ -622,8 +642,8 @@ void launch_query_mlp(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, lo
                       unsigned* words, float* out, hipStream_t s) {
 #define CBN_Q(H, M) launch_query_t<NC, H, M>(pp, grid, ev, Q, QW, L, words, out, s)
     switch (pp->hmax * 8 + pp->mode) {
-        case 16 * 8 + 2: CBN_Q(16, 2); break;
-        case 16 * 8 + 3: CBN_Q(16, 3); break;
+        case 1 * 8 + 2: CBN_Q(1, 2); break;
+        case 1 * 8 + 3: CBN_Q(1, 3); break;
         case 32 * 8 + 2: CBN_Q(32, 2); break;
         default: CBN_Q(32, 3); break;
     }
@@ -841,7 +861,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     if (ok && !consts.empty()) {
         switch (hmax) {
             case 0: launch_const_t<0>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
-            case 16: launch_const_t<16>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
+            case 1: launch_const_t<1>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
             default: launch_const_t<32>(pp->d_image, pp->d_which, (int)consts.size(), N, pp->deep_const, nullptr); break;
         }
         ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
@@ -874,7 +894,7 @@ int cbn_param_eval(const cbn_param_model* model, const float* points, int64_t n_
                        (int)root_bias_only, out)
     switch (hmax_for(m)) {
         case 0: CBN_EVAL(0); break;
-        case 16: CBN_EVAL(16); break;
+        case 1: CBN_EVAL(1); break;
         default: CBN_EVAL(32); break;
     }
 #undef CBN_EVAL

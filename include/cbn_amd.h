@@ -22,7 +22,7 @@ extern "C" {
 #define CBN_AMD_ABI_VERSION 2
 
 #define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
-#define CBN_MAX_EVIDENCE 64  /* distinct evidence columns per query batch        */
+#define CBN_MAX_EVIDENCE 256 /* distinct evidence columns per query batch        */
 
 #define CBN_OK 0
 #define CBN_E_ARG -1

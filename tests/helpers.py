@@ -147,3 +147,25 @@ def alarm_like_data(S, seed, n=37, d=8, max_parents=4, n_edges=46):
     cols = [f"X{i}" for i in range(n)]
     edges = [(f"X{p}", f"X{i}") for i in range(n) for p in sorted(parents[i])]
     return X.astype(np.float32), cols, edges
+
+
+def grid_data(S, seed, side=10, d=64, keep=0.8):
+    """BASELINE configs[4]-shaped network: side x side grid DAG (node (r, c)
+    has parents (r, c-1) and (r-1, c)), d levels per node: X = mean of the
+    parents + small noise (mod d) with probability ``keep``, else uniform."""
+    rng = np.random.default_rng(seed)
+    n = side * side
+    X = np.zeros((S, n), np.int64)
+    edges = []
+    for r in range(side):
+        for c in range(side):
+            i = r * side + c
+            ps = ([i - 1] if c > 0 else []) + ([i - side] if r > 0 else [])
+            edges += [(f"X{p}", f"X{i}") for p in ps]
+            if not ps:
+                X[:, i] = rng.integers(0, d, S)
+                continue
+            base = sum(X[:, p] for p in ps) // len(ps)
+            k = rng.random(S) < keep
+            X[:, i] = np.where(k, (base + rng.integers(-2, 3, S)) % d, rng.integers(0, d, S))
+    return X.astype(np.float32), [f"X{i}" for i in range(n)], edges

@@ -391,3 +391,63 @@ def test_alarm_like_config2_full_batch_properties(gpu):
     ref, _ = OracleBN(edges, cols, data).infer("X35", {k: v[sub] for k, v in ev.items()}, 8)
     scale = p[sub].max() / ref.max()
     np.testing.assert_allclose(p[sub], ref * scale, rtol=2e-5, atol=1e-7)
+
+
+def test_grid_beyond_64_factors_and_evidence_columns(gpu):
+    """configs[4] shape at a size the oracle handles: 9 x 9 grid DAG (81
+    factors, 80 evidence columns -- beyond 64 of both), d = 4, vs the oracle
+    (N = 4: one lane per query, the per-wave offset table of 81 factors does
+    not fit LDS, so this runs the generic kernel); sharded == single call."""
+    from continuousbayesiannetwork_amd.distributed import shard_evidence, sharded_infer
+
+    from helpers import grid_data
+
+    data, cols, edges = grid_data(30000, 2, side=9, d=4, keep=0.9)
+    target, names = cols[-1], cols[:-1]
+    ev = sample_evidence(data, cols, names, 300, 5, missing_frac=0.01)
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ref, rdom = ora.infer(target, ev, 4)
+    pdf, dom = bn.infer(target, _t(ev, gpu), N_max=4)
+    np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
+    np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    evt = _t(ev, gpu)
+    one, _ = sharded_infer(bn, target, evt, N_max=4)
+    np.testing.assert_array_equal(one.cpu().numpy(), pdf.cpu().numpy())
+    for r in range(2):
+        part, _ = sharded_infer(bn, target, shard_evidence(evt, 2, r), N_max=4)
+        assert part.shape[0] == 150
+
+
+def test_grid_fast_path_beyond_64_factors(gpu):
+    """9 x 9 grid, d = N = 32 (4 lanes per query): the fast table kernel with
+    81 factors and 80 evidence columns -- single launch == two launches ==
+    sharded raw launches + scale, bit for bit."""
+    from continuousbayesiannetwork_amd.distributed import shard_evidence
+
+    from helpers import grid_data
+
+    data, cols, edges = grid_data(200000, 4, side=9, d=32, keep=0.97)
+    target, names = cols[-1], cols[:-1]
+    ev = _t(sample_evidence(data, cols, names, 20000, 6), gpu)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    bn.engine.fused = False
+    a, _ = bn.infer(target, ev, N_max=32)
+    a = a.clone()
+    bn.engine.fused = True
+    b, _ = bn.infer(target, ev, N_max=32)
+    torch.cuda.synchronize()
+    bn.engine.check_status()
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    rows, words, scales = [], [], []
+    for r in range(3):
+        res = bn.engine.infer_raw(target, shard_evidence(ev, 3, r), 32)
+        assert res is not None  # fast-path plan
+        o, _, w, sc = res
+        rows.append(o)
+        words.append(w.clone())
+        scales.append(sc)
+    m = torch.stack(words).max(0).values
+    for o, sc in zip(rows, scales):
+        sc(o, m)
+    np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), a.cpu().numpy())

@@ -1,0 +1,64 @@
+"""BASELINE configs[4] on one GPU: 100-node grid DAG (10 x 10, parents left
+and up), d = 64, N_max = 64, BruteForce tables, evidence on the 99 non-target
+nodes, target = the last node (every other node is an ancestor: a 100-factor
+product per query).  The reference's factors for a node whose parents are all
+observed are CPD rows (no marginalisation), so there is no dense d x d
+contraction on this path (no MFMA).  Batches of 65 536 and
+262 144 queries; writes gpurun_out/bench_grid.json."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from continuousbayesiannetwork_amd import BayesianNetwork  # noqa: E402
+from helpers import grid_data, make_bn, sample_evidence  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    d = 64
+    data, cols, edges = grid_data(400_000, 3, side=10, d=d)
+    target, names = cols[-1], cols[:-1]
+    t0 = time.time()
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
+    fit_s = time.time() - t0
+    out = {"workload": f"grid 10x10, {len(edges)} edges, d={d}, N_max={d}, evidence on 99 nodes", "runs": []}
+    for Q in (65536, 262144):
+        batches = [{k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, Q, s).items()}
+                   for s in range(2)]
+        t0 = time.time()
+        pdf, _ = bn.infer(target, batches[0], N_max=d)
+        torch.cuda.synchronize()
+        plan_s = time.time() - t0
+        for b in batches:
+            bn.infer(target, b, N_max=d)
+        torch.cuda.synchronize()
+        K = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(K):
+            bn.infer(target, batches[i % 2], N_max=d)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / K
+        plan = next(iter(bn.engine._plans.values()))
+        lib = bn.engine._fast[(target, tuple(batches[0].keys()), d)].lib if bn.engine._fast else None
+        byt = Q * (4 * len(names) + 4 * d)
+        r = dict(queries=Q, factors=len(plan.factors), us_per_call=round(t * 1e6, 1), queries_per_s=round(Q / t, 1),
+                 effective_GBps=round(byt / t / 1e9, 1), image_MB=round(lib.cbn_plan_table_bytes(plan.handle) / 1e6, 1)
+                 if lib else None, fast_path=bool(lib.cbn_plan_max_words(plan.handle)) if lib else None,
+                 first_call_s=round(plan_s, 2), fit_s=round(fit_s, 1), nonzero_frac=float((pdf > 0).float().mean()))
+        out["runs"].append(r)
+        print(json.dumps(r), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "bench_grid.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
