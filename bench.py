@@ -13,7 +13,10 @@ of evidence values) built once per plan; ``--rebuild-tables`` re-runs that
 build every step, and the default run also reports that figure as
 ``value_rebuild_tables``.  N > 1: the batch grows with N (weak scaling), each rank
 owns 65 536 queries and the ranks exchange the global max with one RCCL
-all-reduce between the two query passes (distributed.sharded_infer).
+all-reduce of the block max words between the raw launch and the in-place
+scale, pipelined so a step's exchange overlaps the next step's launch
+(distributed.ShardedStepper; ``--serial-exchange`` for the unpipelined step,
+``--sharded`` runs that N>1 step at N=1 over a one-rank RCCL communicator).
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` for the dominant
 kernel -- the single-launch fused query kernel at N=1 (the write pass when the
@@ -42,7 +45,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from continuousbayesiannetwork_amd import BayesianNetwork  # noqa: E402
-from continuousbayesiannetwork_amd.distributed import sharded_infer  # noqa: E402
+from continuousbayesiannetwork_amd.distributed import ShardedStepper  # noqa: E402
 from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -79,6 +82,10 @@ def parse():
                     help="distinct evidence batches cycled through (64 x 5 MB > the 256 MB Infinity Cache, so "
                          "evidence is read from HBM, not from a cache warmed by the previous step)")
     ap.add_argument("--two-pass", action="store_true", help="force the two-launch (max, write) path")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the N>1 step (raw launch + RCCL all-reduce + scale, pipelined) even at N=1")
+    ap.add_argument("--serial-exchange", action="store_true",
+                    help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
@@ -109,8 +116,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    sharded = world > 1 or a.sharded
+    if sharded:
         torch.cuda.set_device(local)
+        if "MASTER_ADDR" not in os.environ:  # --sharded outside torch.distributed.run
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"),
+                              RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -131,12 +142,19 @@ def main():
         perm = torch.randperm(Q, generator=g) if b else torch.arange(Q)
         batches.append({k: v[perm].contiguous().to(dev) for k, v in base.items()})
     it = [0]
+    # N>1: one raw launch per step on the compute stream; the all-reduce(MAX)
+    # of the block max words + the in-place scale run on a comm stream, so a
+    # step's exchange overlaps the next step's launch (distributed.ShardedStepper)
+    stepper = ShardedStepper(bn, target, d, depth=1 if a.serial_exchange else 4, force_exchange=sharded)
 
     def step():
         ev = batches[it[0] % len(batches)]
         it[0] += 1
-        if world > 1:
-            return sharded_infer(bn, target, ev, N_max=d)
+        if sharded:
+            rows = stepper.step(ev)
+            if a.serial_exchange:
+                stepper.wait()
+            return rows
         return bn.infer(target, ev, N_max=d)
 
     random.seed(0)
@@ -146,20 +164,21 @@ def main():
 
     K = a.steps
     bn.engine.timing()  # drop warm-up timings
-    fused = world == 1 and not a.two_pass and bn.engine.fused_capacity(target, names, d) >= Q
+    fused = not sharded and not a.two_pass and bn.engine.fused_capacity(target, names, d) >= Q
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()  # the library launches on torch's current stream: these events bracket every launch
     for i in range(K):
         # two-launch path: HIP events recorded inside the library around the passes of every 8th step
-        bn.engine.timed = world == 1 and not fused and i % 8 == 7
+        bn.engine.timed = not sharded and not fused and i % 8 == 7
         step()
+    stepper.wait()
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     t1 = time.perf_counter()
     bn.engine.timed = False
@@ -171,7 +190,7 @@ def main():
     value = Q * world * K / sec
 
     roofline = None
-    ntimed, tmax_ms, twrite_ms = bn.engine.timing() if world == 1 else (0, 0.0, 0.0)
+    ntimed, tmax_ms, twrite_ms = bn.engine.timing() if not sharded else (0, 0.0, 0.0)
     bn.engine.check_status()
     if fused:
         # one launch per step: average launch duration = HIP-event time of the timed region / K
@@ -198,7 +217,7 @@ def main():
             roofline["max_pass_us"] = round(tmax * 1e6, 2)
 
     cold = None
-    if world == 1 and not a.rebuild_tables:
+    if not sharded and not a.rebuild_tables:
         bn.engine.cache_tables = False
         for _ in range(5):
             step()
@@ -212,7 +231,7 @@ def main():
         bn.engine.cache_tables = True
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not sharded and not a.no_cpu_baseline:
         cpu = cpu_baseline(data, cols, edges, ev_np, target, d, a.cpu_seconds)
 
     if rank == 0:
@@ -223,7 +242,10 @@ def main():
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded chain samples; BruteForce fit)",
             "config": {"workload": f"chain{n}_d{d}: BayesianNetwork.infer target {target}, evidence on the other "
                                    f"{n - 1} nodes, N_max={d}", "queries_per_gpu": Q, "global_batch": Q * world,
-                       "parallelism": f"query-shard x{world}" + (" + RCCL all-reduce(max)" if world > 1 else "")},
+                       "parallelism": f"query-shard x{world}" + (
+                           " + RCCL all-reduce(max) of the block max words" + (
+                               ", serial" if a.serial_exchange else ", overlapped with the next step's launch")
+                           if sharded else "")},
             "roofline": roofline, "cpu_baseline": cpu,
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
             "evidence_batches": len(batches),
@@ -233,7 +255,8 @@ def main():
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
+        stepper.close()
         dist.destroy_process_group()
 
 

@@ -101,3 +101,103 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
 
     res = normalise_across_ranks(local_max, local_write, group=group, gather=gather)
     return res, tdom
+
+
+class ShardedStepper:
+    """Pipelined ``sharded_infer`` for a stream of query batches (serving /
+    the multi-GPU bench): step i's exchange overlaps step i+1's raw launch.
+
+    Per step, in ONE native host call (``_cbn_host.Stepper``): on the caller's
+    (compute) stream, ONE raw launch (unnormalised rows + per-block max words
+    into a ring slot) and an event; on the stepper's comm stream, wait for that
+    event, ``ncclAllReduce(MAX)`` of the words on our own RCCL communicator,
+    scale the rows in place, mark the slot free.  The compute stream waits for
+    the exchange only to reuse a ring slot ``depth`` steps later, so the RCCL
+    latency hides behind the next batch's launch.  (The same choreography in
+    Python -- events, stream switch, c10d all_reduce, record_stream -- cost
+    ~50 us of host time per step: tools/shard_step_probe.py.)
+
+    The returned rows are complete once the comm stream has run the step's
+    scale: call ``wait()`` (the current stream waits for the comm stream)
+    before reading them on another stream.  Results equal ``sharded_infer``
+    (and the single-process ``infer`` on the concatenated batch) bit for bit.
+    Every rank must call ``step`` the same number of times (one collective per
+    step).  Plans without a raw launch, and evidence the native checks reject,
+    fall back to the serial ``sharded_infer`` (c10d collectives).
+    """
+
+    def __init__(self, bn, target_node: str, N_max: int = 16, group=None, depth: int = 4,
+                 force_exchange: bool = False):
+        self.bn, self.target, self.N_max, self.group = bn, target_node, N_max, group
+        self.depth = max(1, depth)
+        # force_exchange: all-reduce even at world size 1 (exercises RCCL on one GPU)
+        self.exchange = force_exchange or (dist.is_initialized() and dist.get_world_size(group) > 1)
+        self._c = None
+        self._fp = None
+        self._comm = 0
+
+    def _setup(self, evidence_shard) -> bool:
+        import os
+
+        from . import _native
+
+        fp = self.bn.engine.raw_fast_path(self.target, evidence_shard, self.N_max)
+        if fp is None:
+            return False
+        host = _native.load_host()
+        if self.exchange:
+            rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+            if dist.is_initialized():
+                world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+                obj = [host.nccl_unique_id(rccl) if rank == 0 else None]
+                src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+                dist.broadcast_object_list(obj, src=src, group=self.group)
+                uid = obj[0]
+            else:
+                world, rank, uid = 1, 0, host.nccl_unique_id(rccl)
+            self._comm = host.nccl_comm_init(rccl, uid, world, rank, fp.device.index)
+        plan = fp.plan
+        self._c = host.Stepper(fp.run_fn, fp.scale_fn, plan.handle.value, fp.slot_keys, fp.first, fp.device.index,
+                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.depth, self._comm)
+        self._fp = fp
+        return True
+
+    def step(self, evidence_shard: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None):
+        if self._c is None and not self._setup(evidence_shard):
+            return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, out=out)
+        fp = self._fp
+        res = self._c.step(evidence_shard, out, self.bn.engine.raw_flags(fp.plan))
+        if res is None:
+            self.wait()
+            return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, out=out)
+        if type(res) is int:
+            from . import _native
+
+            _native.check(res, "cbn_plan_run(raw)")
+        n = res.shape[0]
+        tdom = fp.tdom.get(n)
+        if tdom is None:
+            plan = fp.plan
+            tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
+        return res, tdom
+
+    def wait(self):
+        """Make the current stream wait for every enqueued exchange + scale."""
+        if self._c is not None:
+            self._c.wait()
+
+    def synchronize(self):
+        if self._c is not None:
+            self._c.synchronize()
+
+    def close(self):
+        """Drain the comm stream and destroy the RCCL communicator (collective:
+        every rank calls it)."""
+        if self._c is not None:
+            self._c.synchronize()
+            self._c = None
+        if self._comm:
+            from . import _native
+
+            _native.load_host().nccl_comm_destroy(self._comm)
+            self._comm = 0

@@ -345,7 +345,7 @@ class InferenceEngine:
                 plan.destroy()
 
     def infer_raw(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int,
-                  out: Optional[torch.Tensor] = None):
+                  out: Optional[torch.Tensor] = None, words: Optional[torch.Tensor] = None):
         """One launch storing this batch's UNnormalised rows (the factor product
         of bayesian_network.py:269-295) and its max word -- the per-rank step of
         the sharded path, which all-reduces the word and then calls the returned
@@ -354,24 +354,21 @@ class InferenceEngine:
         Returns (rows, target domain, max words int32[W], scale) or None when
         the plan cannot take a raw launch (the caller uses the two-pass
         exchange).  The W words are per-block maxima (all-reduce them with MAX).
+        ``words``: a caller-owned int32[W] buffer for them (W =
+        ``raw_word_count``); by default the plan's own buffer, which the next
+        raw launch of the same plan overwrites.
         """
-        key = (target, tuple(evidence.keys()), N_max)
-        fp = self._fast.get(key)
+        fp = self.raw_fast_path(target, evidence, N_max)
         if fp is None:
-            device = _native.require_gpu(self.bn.device)
-            if len(evidence) == 0:
-                return None
-            observed = relevant_observed(self.bn, self._order(target), evidence.keys())
-            plan = self.plan(target, observed, N_max, device)
-            if not plan.deterministic:
-                plan.destroy()
-                return None
-            fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
-        plan = fp.plan
-        if fp.words is None:
             return None
+        plan = fp.plan
+        if words is None:
+            words = fp.words
+        elif (words.dtype is not torch.int32 or words.device != fp.device or words.numel() != fp.words.numel()
+              or not words.is_contiguous()):
+            raise ValueError(f"words must be a contiguous int32[{fp.words.numel()}] tensor on {fp.device}")
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
-                      plan.n_samples, plan.target_observed, fp.words.data_ptr(),
+                      plan.n_samples, plan.target_observed, words.data_ptr(),
                       self._flags(plan) | _native.CBN_RUN_RAW, out)
         if res is None or (type(res) is int and res == _native.CBN_E_UNSUPPORTED):
             return None
@@ -388,7 +385,33 @@ class InferenceEngine:
                 _native.check(rc, "cbn_scale")
             return rows
 
-        return res, tdom, fp.words, scale
+        return res, tdom, words, scale
+
+    def raw_fast_path(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int) -> Optional["_FastPath"]:
+        """The cached fast path of (target, evidence keys, N) when its plan takes
+        raw launches (planned here if needed, nothing launched); else None."""
+        key = (target, tuple(evidence.keys()), N_max)
+        fp = self._fast.get(key)
+        if fp is None:
+            device = _native.require_gpu(self.bn.device)
+            if len(evidence) == 0:
+                return None
+            observed = relevant_observed(self.bn, self._order(target), evidence.keys())
+            plan = self.plan(target, observed, N_max, device)
+            if not plan.deterministic:
+                plan.destroy()
+                return None
+            fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
+        return fp if fp.words is not None else None
+
+    def raw_flags(self, plan: Plan) -> int:
+        return self._flags(plan) | _native.CBN_RUN_RAW
+
+    def raw_word_count(self, target: str, evidence_keys, N_max: int) -> int:
+        """W, the number of per-block max words of this (target, evidence keys,
+        N) raw launch; 0 when it has none (or no raw launch ran yet)."""
+        fp = self._fast.get((target, tuple(evidence_keys), N_max))
+        return 0 if fp is None or fp.words is None else int(fp.words.numel())
 
     def _flags(self, plan: Plan) -> int:
         f = 0

@@ -308,6 +308,34 @@ def test_raw_launch_sharded_equals_single_launch(Q, shards, gpu):
     np.testing.assert_array_equal(one.cpu().numpy(), full.cpu().numpy())
 
 
+@pytest.mark.parametrize("depth,exchange", [(1, False), (2, True), (4, False), (4, True)])
+def test_sharded_stepper_pipelined_equals_infer(depth, exchange, gpu):
+    """ShardedStepper (raw launch on the compute stream, exchange + scale on
+    its comm stream, ring of max-word buffers) over a stream of distinct
+    batches == infer on each batch, bit for bit -- including rows released
+    early (the allocator must not recycle them before the comm stream's scale)."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper
+
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    batches = [_t(sample_evidence(data, cols, names, 4096 + 1000 * i, 30 + i), gpu) for i in range(7)]
+    ref = [bn.infer("X19", b, N_max=32)[0].clone() for b in batches]
+    # exchange: a one-rank RCCL communicator of the stepper's own (no process group)
+    st = ShardedStepper(bn, "X19", 32, depth=depth, force_exchange=exchange)
+    keep = []
+    for rep in range(3):
+        for i, b in enumerate(batches):
+            rows, dom = st.step(b)
+            if i % 2 == 0:
+                keep.append((i, rows))  # odd steps' rows are dropped right away
+    st.wait()
+    torch.cuda.synchronize()
+    st.close()
+    for i, rows in keep:
+        np.testing.assert_array_equal(rows.cpu().numpy(), ref[i].cpu().numpy())
+
+
 def test_raw_launch_unsupported_plan_falls_back(gpu):
     """Plans off the fast path (a factor with > 4 observed parents) run the
     two-pass exchange."""

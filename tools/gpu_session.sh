@@ -20,7 +20,7 @@ step() {
 }
 for s in "$@"; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfast) step bench 600 python bench.py --no-cpu-baseline ;;
@@ -29,6 +29,11 @@ for s in "$@"; do
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline &&
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline ;;
     summary) step summary 120 python tools/profile_summary.py --tag "${TAG:-r01}" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 40)" ;;
+    stepper) step pytest_stepper 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "stepper or raw_launch" --timeout 120 --timeout-method thread ;;
+    probe) step shard_probe 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 tools/shard_step_probe.py ;;
+    benchsharded) step bench_sharded 300 python bench.py --no-cpu-baseline --sharded ;;
+    benchserial) step bench_serial 300 python bench.py --no-cpu-baseline --sharded --serial-exchange ;;
+    torchrun1) step bench_torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 1 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
