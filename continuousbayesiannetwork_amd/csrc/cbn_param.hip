@@ -94,12 +94,45 @@ __device__ __forceinline__ unsigned wave_max_u(unsigned v) {
     return v;
 }
 
+// n / d to within one ulp of the correctly rounded quotient: v_rcp_f32 + one
+// Newton step (4 VALU slots instead of the ~12 of the IEEE division
+// sequence).  v_rcp_f32 flushes reciprocals below 2^-126, so denominators
+// above 2^126 (a logistic (1 + e)^2 near FLT_MAX), inf and NaN take the IEEE
+// division -- a branch no lane takes in range, skipped by the whole wave.
+__device__ __forceinline__ float div_nr(float n, float d, float r) {
+    const float q = n * r;
+    float res = fmaf(fmaf(-d, q, n), r, q);
+    if (!(d <= 0x1p126f)) res = n / d;
+    return res;
+}
+__device__ __forceinline__ float div_nr(float n, float d) { return div_nr(n, d, __builtin_amdgcn_rcpf(d)); }
+
+// exp(x) within ~2 ulp for results >= 2^-126 in 7 VALU slots (libm expf: 13):
+// x log2(e) = hi + lo exactly (product residual by fma, plus x times the
+// low part of log2(e)), 2^hi by v_exp_f32, 2^lo ~ 1 + lo ln2 (|lo| <= 2^-24
+// |hi|).  x below -104 (exp underflows) is clamped so the residual stays
+// finite; NaN passes through (comparisons false).  v_exp_f32 returns 0 where
+// 2^hi is subnormal (hi < -126): such a density is < 1.2e-38 and flushes to
+// 0 (the reference keeps the subnormal) -- measured and bounded in
+// tests/test_gpu_param.py::test_density_accuracy_full_range.
+__device__ __forceinline__ float exp_split(float x) {
+    constexpr float kL = 1.44269502162933349609375f;  // fp32(log2 e)
+    constexpr float kLlo = 1.925963033500e-8f;       // log2 e - kL
+    constexpr float kLn2 = 0.693147180559945309f;
+    x = x < -104.f ? -104.f : x;
+    const float ph = x * kL;
+    const float pl = fmaf(x, kLlo, fmaf(x, kL, -ph));
+    const float r = __builtin_amdgcn_exp2f(ph);
+    return fmaf(r, pl * kLn2, r);
+}
+
 // activation_map of neural_network.py:10-18 (torch CPU formulas)
 __device__ __forceinline__ float act1(int act, float x) {
     switch (act) {
         case CBN_ACT_TANH: return tanhf(x);
         case CBN_ACT_RELU: return x > 0.f ? x : 0.f;
-        case CBN_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+        case CBN_ACT_SIGMOID:  // exp(-x) clamped below FLT_MAX: 1 / (1 + 3.3e38) for x < -88.7 (torch: 0)
+            return div_nr(1.f, 1.f + exp_split(-x > 88.7f ? 88.7f : -x));  // NaN stays NaN
         case CBN_ACT_LEAKYRELU: return x > 0.f ? x : x * 0.01f;
         case CBN_ACT_GELU: return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
         case CBN_ACT_ELU: return x > 0.f ? x : expm1f(x);
@@ -131,6 +164,41 @@ __device__ __forceinline__ void activate(int act, int w, float (&h)[H]) {
     }
 }
 
+// One hidden layer (the reference's default, neural_network.py:37): stream
+// over the hidden units -- mu = b2 + sum_o W2[o] act(W1[o] . z + b1[o]) in o
+// order (the output layer's fma chain) -- four units per step, so the
+// wave-uniform weight reads of a step are issued together (scalar loads) and
+// their latency is paid once per four units.  ACT 0: runtime activation.
+template <int ACT>
+__device__ __forceinline__ float mlp1(const float* __restrict__ W, int n_in, int H, const float (&z)[kMaxP],
+                                      int act = ACT) {
+    const float* B1 = W + H * n_in;
+    const float* W2 = B1 + H;
+    float mu = 0.f;
+    int o = 0;
+    for (; o + 4 <= H; o += 4) {
+        float s[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float a = 0.f;
+#pragma unroll
+            for (int i = 0; i < kMaxP; ++i)
+                if (i < n_in) a = fmaf(W[(o + u) * n_in + i], z[i], a);
+            s[u] = a + B1[o + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mu = fmaf(W2[o + u], act1(act, s[u]), mu);
+    }
+    for (; o < H; ++o) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < kMaxP; ++i)
+            if (i < n_in) a = fmaf(W[o * n_in + i], z[i], a);
+        mu = fmaf(W2[o], act1(act, a + B1[o]), mu);
+    }
+    return mu + W2[H];
+}
+
 // mu = model(z): y = W x + b per nn.Linear (dot product first, then the bias:
 // addmm's order), activation after every layer but the last.  HMAX = 0: the
 // linear-model instantiation (n_layers == 1 only).  The first hidden layer
@@ -148,22 +216,13 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
             if (i < n_in) s = fmaf(W[i], z[i], s);
         return s + W[n_in];
     } else if (HMAX == 1 || m.n_layers == 2) {
-        // one hidden layer (the reference's default, neural_network.py:37):
-        // stream over the hidden units -- mu = b2 + sum_o W2[o] act(W1[o] . z + b1[o])
-        // in o order, the same fma chain as the output layer's dot product, with
-        // only a handful of weights live at a time
-        const int H = m.width[1];
-        const float* B1 = W + H * n_in;
-        const float* W2 = B1 + H;
-        float mu = 0.f;
-        for (int o = 0; o < H; ++o) {
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < kMaxP; ++i)
-                if (i < n_in) s = fmaf(W[o * n_in + i], z[i], s);
-            mu = fmaf(W2[o], act1(m.act, s + B1[o]), mu);
+        switch (m.act) {  // wave-uniform: one branch per model evaluation, not per unit
+            case CBN_ACT_TANH: return mlp1<CBN_ACT_TANH>(W, n_in, m.width[1], z);
+            case CBN_ACT_RELU: return mlp1<CBN_ACT_RELU>(W, n_in, m.width[1], z);
+            case CBN_ACT_SIGMOID: return mlp1<CBN_ACT_SIGMOID>(W, n_in, m.width[1], z);
+            case CBN_ACT_LEAKYRELU: return mlp1<CBN_ACT_LEAKYRELU>(W, n_in, m.width[1], z);
+            default: return mlp1<0>(W, n_in, m.width[1], z, m.act);
         }
-        return mu + W2[H];
     } else {
         constexpr int H = HMAX > 1 ? HMAX : 1;
         float h[H];
@@ -210,38 +269,6 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
             if (i < win) s = fmaf(W[i], h[i], s);
         return s + W[win];
     }
-}
-
-// n / d to within one ulp of the correctly rounded quotient: v_rcp_f32 + one
-// Newton step (4 VALU slots instead of the ~12 of the IEEE division
-// sequence).  v_rcp_f32 flushes reciprocals below 2^-126, so denominators
-// above 2^126 (a logistic (1 + e)^2 near FLT_MAX), inf and NaN take the IEEE
-// division -- a branch no lane takes in range, skipped by the whole wave.
-__device__ __forceinline__ float div_nr(float n, float d, float r) {
-    const float q = n * r;
-    float res = fmaf(fmaf(-d, q, n), r, q);
-    if (!(d <= 0x1p126f)) res = n / d;
-    return res;
-}
-__device__ __forceinline__ float div_nr(float n, float d) { return div_nr(n, d, __builtin_amdgcn_rcpf(d)); }
-
-// exp(x) within ~2 ulp for results >= 2^-126 in 7 VALU slots (libm expf: 13):
-// x log2(e) = hi + lo exactly (product residual by fma, plus x times the
-// low part of log2(e)), 2^hi by v_exp_f32, 2^lo ~ 1 + lo ln2 (|lo| <= 2^-24
-// |hi|).  x below -104 (exp underflows) is clamped so the residual stays
-// finite; NaN passes through (comparisons false).  v_exp_f32 returns 0 where
-// 2^hi is subnormal (hi < -126): such a density is < 1.2e-38 and flushes to
-// 0 (the reference keeps the subnormal) -- measured and bounded in
-// tests/test_gpu_param.py::test_density_accuracy_full_range.
-__device__ __forceinline__ float exp_split(float x) {
-    constexpr float kL = 1.44269502162933349609375f;  // fp32(log2 e)
-    constexpr float kLlo = 1.925963033500e-8f;       // log2 e - kL
-    constexpr float kLn2 = 0.693147180559945309f;
-    x = x < -104.f ? -104.f : x;
-    const float ph = x * kL;
-    const float pl = fmaf(x, kLlo, fmaf(x, kL, -ph));
-    const float r = __builtin_amdgcn_exp2f(ph);
-    return fmaf(r, pl * kLn2, r);
 }
 
 // Densities, in the reference's fp32 operation order (divisions within one
@@ -341,10 +368,23 @@ __device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, long long 
 // UNnormalised rows and one max word per block (the global-max division of
 // bayesian_network.py:296 runs after, in k_scale, possibly after a cross-rank
 // all-reduce of the words).
+// Factor split: a block's 8 waves = (8 / parts) query groups x `parts`
+// contiguous factor ranges [f[p], f[p + 1]) (balanced by estimated cost on
+// the host).  Wave (group g, part p) multiplies its range's factors for the
+// group's 64 queries; parts 1.. leave their products in LDS (comb_off floats
+// into the dynamic LDS), part 0 multiplies them in (part order) and writes.
+// Batches too small to give every SIMD several waves (131 072 queries of an
+// MLP: 2 048 waves for 1 024 SIMDs) run 2-4 parts.
+struct FSplit {
+    int parts;
+    int comb_off;
+    int f[5];
+};
+
 template <int NC, int HMAX, int MODE, bool TAB>
 __global__ void __launch_bounds__(kQThreads)
 k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
-              int n_words, unsigned* __restrict__ max_out, float* __restrict__ out) {
+              int n_words, unsigned* __restrict__ max_out, float* __restrict__ out, FSplit sp) {
     const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);
     // dynamic LDS: [nf x kMaxP InCol] [deep-model scratch, models with >= 2 hidden layers]
     extern __shared__ __attribute__((aligned(16))) float4 smem_q[];
@@ -365,9 +405,17 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
     const int wpb = kQThreads / kWave;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int tasks = QW * L;
+    const int parts = sp.parts;
+    const int gpb = wpb / parts;  // query groups per block
+    const int part = wid % parts, grp = wid / parts;
+    const int f0 = sp.f[part], f1 = sp.f[part + 1];
+    float* comb = reinterpret_cast<float*>(smem_q) + sp.comb_off;  // [wpb][NC][64]
     float lmax = 0.f;
-    for (int t = blockIdx.x * wpb + wid; t < tasks; t += gridDim.x * wpb) {
-        const int l = t / QW;
+    // block-uniform trip count (the combine step has block barriers)
+    for (int tb = blockIdx.x * gpb; tb < tasks; tb += gridDim.x * gpb) {
+        const int t = tb + grp;
+        const bool active = t < tasks;
+        const int l = (active ? t : tasks - 1) / QW;
         const long long q = (long long)(t - l * QW) * kWave + lane;
         const bool valid = q < Q;
         const long long qs = valid ? q : Q - 1;
@@ -377,12 +425,13 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
-        if (TAB) load_inputs_tab(ev, 0, qs, z);
-        else load_inputs(incol, qs, z);
-        for (int f = 0; f < nf; ++f) {
+        const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
+        if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qs, z);
+        else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
+        for (int f = fa; f < f1; ++f) {
             const PRec& r = rec[f];
             float zn[kMaxP];
-            const int fn = f + 1 < nf ? f + 1 : f;  // next factor's evidence in flight during this one
+            const int fn = f + 1 < f1 ? f + 1 : f;  // next factor's evidence in flight during this one
             if (TAB) load_inputs_tab(ev, fn, qs, zn);
             else load_inputs(incol + fn * kMaxP, qs, zn);
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
@@ -431,7 +480,22 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
             for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
         }
-        if (valid) {
+        if (parts > 1) {
+            float* mine = comb + (wid * NC) * kWave + lane;
+            if (part != 0 && active) {
+#pragma unroll
+                for (int j = 0; j < NC; ++j) mine[j * kWave] = acc[j];
+            }
+            __syncthreads();
+            if (part == 0 && active) {
+                for (int p = 1; p < parts; ++p) {
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                }
+            }
+            __syncthreads();
+        }
+        if (part == 0 && active && valid) {
             float* o = out + q * N + col0;
             if ((N & 3) == 0 && (NC & 3) == 0 && ncol == NC) {
 #pragma unroll
@@ -594,9 +658,6 @@ void launch_const_t(float* img, const int* which, int n, int N, size_t lds, hipS
     hipLaunchKernelGGL(k_param_const<HMAX>, dim3(n), dim3(kThreads), lds, s, img, which, N);
 }
 
-template <int NC, int HMAX>
-void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, long long QW,
-                    unsigned* words, float* out, hipStream_t s);
 
 }  // namespace
 
@@ -615,6 +676,7 @@ struct ParamPlan {
     size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
     size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
+    int split[3][5] = {};  // factor ranges for 1 / 2 / 4 parts (index parts >> 1)
     float* d_image = nullptr;
     int* d_which = nullptr;
     int image_floats = 0;
@@ -624,11 +686,18 @@ struct ParamPlan {
 namespace {
 template <int NC, int HMAX, int MODE, bool TAB = (MODE < 4)>
 void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
-                    unsigned* words, float* out, hipStream_t s) {
+                    unsigned* words, float* out, hipStream_t s, int parts) {
     allow_deep(&k_param_query<NC, HMAX, MODE, TAB>);
-    const size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
+    FSplit sp;
+    memset(&sp, 0, sizeof(sp));
+    sp.parts = parts;
+    for (int p = 0; p <= parts; ++p) sp.f[p] = pp->split[parts >> 1][p];
+    size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
+    lds = (lds + 15) & ~(size_t)15;
+    sp.comb_off = (int)(lds / sizeof(float));
+    if (parts > 1) lds += (size_t)(kQThreads / kWave) * NC * kWave * sizeof(float);
     hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
-                       pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out);
+                       pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out, sp);
 }
 
 // Instantiated (HMAX, MODE) pairs: linear models (HMAX 0) of either family,
@@ -639,8 +708,8 @@ bool specialised(int hmax, int mode) { return mode < 4 && (hmax == 0 || mode >= 
 // MLP (NeuralNetwork, logistic density) kernels for one column chunk
 template <int NC>
 void launch_query_mlp(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
-                      unsigned* words, float* out, hipStream_t s) {
-#define CBN_Q(H, M) launch_query_t<NC, H, M>(pp, grid, ev, Q, QW, L, words, out, s)
+                      unsigned* words, float* out, hipStream_t s, int parts) {
+#define CBN_Q(H, M) launch_query_t<NC, H, M>(pp, grid, ev, Q, QW, L, words, out, s, parts)
     switch (pp->hmax * 8 + pp->mode) {
         case 1 * 8 + 2: CBN_Q(1, 2); break;
         case 1 * 8 + 3: CBN_Q(1, 3); break;
@@ -688,24 +757,34 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     const int L = (pp->N + nc - 1) / nc;
     const long long waves = QW * L;
     if (waves >= (1LL << 31)) return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
-    long long grid = (waves + kQThreads / kWave - 1) / (kQThreads / kWave);
+    // factor split: a plan constant (never a function of the batch size), so
+    // the product order -- and every row bit -- is the same however the batch
+    // is sharded.  Two parts: configs[3] NN [16] at 131 072 queries 304 -> 218
+    // us, LR and 1 M-query batches unchanged within noise (4 parts: 215 us at
+    // 131 072, 2 % slower at 1 M), profiles/r01_bench_cont.json.
+    int parts = pp->nf >= 2 ? 2 : 1;
+    if (const char* e = getenv("CBN_PARAM_PARTS")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) parts = v;
+    }
+    long long grid = (waves * parts + kQThreads / kWave - 1) / (kQThreads / kWave);
     grid = std::max(1LL, std::min(grid, (long long)pp->max_slots));
     const bool raw = (flags & CBN_RUN_RAW) != 0;
     unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
     if (!specialised(pp->hmax, pp->mode)) {
-        launch_query_t<16, 32, 4>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s);
+        launch_query_t<16, 32, 4>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
     } else if (pp->hmax == 0) {  // linear models: 8-column chunks
         switch (pp->mode) {
-            case 0: launch_query_t<8, 0, 0>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
-            case 1: launch_query_t<8, 0, 1>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
-            case 2: launch_query_t<8, 0, 2>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
-            default: launch_query_t<8, 0, 3>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            case 0: launch_query_t<8, 0, 0>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
+            case 1: launch_query_t<8, 0, 1>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
+            case 2: launch_query_t<8, 0, 2>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
+            default: launch_query_t<8, 0, 3>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
         }
     } else {
         switch (nc) {
-            case 8: launch_query_mlp<8>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
-            case 16: launch_query_mlp<16>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
-            default: launch_query_mlp<32>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s); break;
+            case 8: launch_query_mlp<8>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
+            case 16: launch_query_mlp<16>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
+            default: launch_query_mlp<32>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
         }
     }
     PHIP_TRY(hipGetLastError());
@@ -831,6 +910,32 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     pp->nc = nc;
     pp->L = (N + nc - 1) / nc;
     pp->max_slots = std::min(4 * num_cu(), kMaxSlots);
+    {   // factor ranges of the split query kernel, balanced by estimated VALU cost
+        std::vector<double> cost(n_factors, 1.0);
+        double total = 0;
+        for (int f = 0; f < n_factors; ++f) {
+            const PRec& r = recs[f];
+            if (r.kind == CBN_FACTOR_QUERY) {
+                double mc = 0;
+                for (int l = 0; l < r.m.n_layers; ++l) mc += (double)r.m.width[l + 1] * (r.m.width[l] + 1);
+                for (int l = 1; l < r.m.n_layers; ++l) mc += 20.0 * r.m.width[l];  // activations
+                cost[f] = (double)r.M * (mc + 15.0 * N);
+            }
+            total += cost[f];
+        }
+        for (int k = 0; k < 3; ++k) {
+            const int parts = 1 << k;
+            int* b = pp->split[k];
+            b[0] = 0;
+            int p = 1;
+            double acc = 0;
+            for (int f = 0; f < n_factors && p < parts; ++f) {
+                acc += cost[f];
+                while (p < parts && acc >= total * p / parts) b[p++] = f + 1;
+            }
+            while (p <= parts) b[p++] = n_factors;
+        }
+    }
     cbn_plan* P = new cbn_plan();
     P->param = pp;
     P->nf = n_factors;

@@ -299,3 +299,46 @@ def test_density_accuracy_full_range(gpu):
         normal = ~nan & ~zero & (ideal >= tiny)  # zero: the reference's (1 + e)^2 overflowed
         ulp = np.abs(got[normal].astype(np.float64) - ideal[normal]) / np.spacing(ideal[normal])
         assert ulp.max() <= 4, (ls, ulp.max())
+
+
+@pytest.mark.parametrize("act", ["tanh", "sigmoid"])
+def test_activation_accuracy(act, gpu):
+    """The kernels' tanh (ocml tanhf) and sigmoid (split exp + Newton-refined
+    reciprocal) vs float64,
+    through cbn_param_eval of mu = act(x) (one hidden unit, W = 1, b = 0) and a
+    Gaussian at the point 0: pdf = exp(-0.5 (mu / s)^2), so mu = s sqrt(-2 ln
+    pdf) recovers mu to ~1 ulp when s puts (mu / s)^2 in [36, 150] (one call
+    per binade of mu).  Bound: 8 ulp of the float64 activation."""
+    import ctypes
+
+    from continuousbayesiannetwork_amd import _native
+
+    lib = _native.load()
+    x = np.concatenate([np.linspace(-9, 9, 400001), np.logspace(-7, 0.5, 20001), -np.logspace(-7, 0.5, 20001)])
+    x = x.astype(np.float32)
+    x64 = x.astype(np.float64)
+    ref = np.tanh(x64) if act == "tanh" else 1 / (1 + np.exp(-x64))
+    keep = ref != 0
+    x, ref = x[keep], ref[keep]
+    code = _native.CBN_ACT[act]
+    w = torch.tensor([1.0, 0.0, 1.0, 0.0], device=gpu)
+    worst = 0.0
+    binade = np.floor(np.log2(np.abs(ref)))
+    for b in np.unique(binade):
+        sel = binade == b
+        s = np.float32(2.0 ** b / 6)  # (mu / s)^2 in [36, 144)
+        m = _native.ParamModel()
+        m.family, m.n_layers, m.act = _native.CBN_FAMILY_GAUSS, 2, code
+        m.width[0], m.width[1], m.width[2] = 1, 1, 1
+        m.weights, m.scale, m.norm = w.data_ptr(), float(s), 1.0
+        q = torch.tensor(x[sel][:, None], device=gpu)
+        pts = torch.zeros((q.shape[0], 1), device=gpu)
+        out = torch.empty_like(pts)
+        _native.check(lib.cbn_param_eval(ctypes.byref(m), _native.ptr(pts), q.shape[0], 1, _native.ptr(q), 0,
+                                         _native.ptr(out), _native.stream_ptr(gpu)), "cbn_param_eval")
+        pdf = out.cpu().numpy()[:, 0].astype(np.float64)
+        mu = np.float64(s) * np.sqrt(-2 * np.log(pdf))
+        r = ref[sel]
+        ulp = np.abs(mu - np.abs(r)) / np.spacing(np.abs(r).astype(np.float32))
+        worst = max(worst, float(ulp.max()))
+    assert worst <= 8, worst

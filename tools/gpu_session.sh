@@ -34,6 +34,10 @@ for s in "$@"; do
     benchsharded) step bench_sharded 300 python bench.py --no-cpu-baseline --sharded ;;
     benchserial) step bench_serial 300 python bench.py --no-cpu-baseline --sharded --serial-exchange ;;
     torchrun1) step bench_torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 1 --no-cpu-baseline ;;
+    param) step pytest_param 400 python -u -m pytest tests/test_gpu_param.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    cont) step bench_cont 400 python tools/bench_cont.py ;;
+    alarm) step bench_alarm 400 python tools/bench_alarm.py ;;
+    grid) step bench_grid 600 python tools/bench_grid.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
