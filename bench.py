@@ -143,9 +143,10 @@ def main():
         batches.append({k: v[perm].contiguous().to(dev) for k, v in base.items()})
     it = [0]
     # N>1: one raw launch per step on the compute stream; the all-reduce(MAX)
-    # of the block max words + the in-place scale run on a comm stream, so a
-    # step's exchange overlaps the next step's launch (distributed.ShardedStepper)
-    stepper = ShardedStepper(bn, target, d, depth=1 if a.serial_exchange else 4, force_exchange=sharded)
+    # of the block max words + the in-place scale run on a comm stream, once per
+    # 4 steps for all 4, so the exchange overlaps the next steps' launches
+    # (distributed.ShardedStepper)
+    stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else 4, force_exchange=sharded)
 
     def step():
         ev = batches[it[0] % len(batches)]
@@ -201,7 +202,8 @@ def main():
         bytes_write = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
         achieved = bytes_write / twrite / 1e9
         vpl = int(os.environ.get("CBN_FAST_VPL", "2"))
-        kname = f"k_query_fast<{vpl}, true, {2 if fused else 1}>"  # <VPL, LDS, MODE 2 fused / 1 write>
+        nptr = 128 if 4 * n <= 128 else 416  # kernel-argument pointer table sized to the plan (n factors)
+        kname = f"k_query_fast<{vpl}, true, {2 if fused else 1}, {nptr}>"  # <VPL, LDS, MODE 2 fused / 1 write, NP>
         traffic, tsrc = pmc_traffic(kname)
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,

@@ -104,6 +104,8 @@ _SIGNATURES = {
     "cbn_plan_fused_capacity": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    "cbn_scale_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_int32, ctypes.c_void_p]),
     "cbn_plan_max_words": (ctypes.c_int32, [ctypes.c_void_p]),
     "cbn_plan_create_param": (ctypes.c_int, [ctypes.POINTER(ParamFactor), ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_void_p)]),

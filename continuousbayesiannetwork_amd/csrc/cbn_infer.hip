@@ -110,8 +110,13 @@ struct EvPtrs {
 // kTagNone = no observed parent (a valid dummy column, read at row 0), so the
 // first-parent loads of all a lane's factors issue back to back, unbranched.
 constexpr uintptr_t kTagMore = 1, kTagNone = 2;
-struct FPtrs {
-    const float* p[kFastPtrs];
+// Kernel arguments are copied per launch: plans of <= 32 factors (configs[1],
+// [2]) take a 1 KiB table (launch 3.2 us of host time instead of 4.9 us with
+// the 3.3 KiB one, profiles/r01_launch_cost.txt).
+constexpr int kFastPtrsSmall = 128;
+template <int NP>
+struct FPtrsT {
+    const float* p[NP];
 };
 
 struct ColPtrs {
@@ -519,9 +524,9 @@ constexpr int kLoc = 8;
 constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
-template <int VPL, bool USE_LDS, int MODE>
+template <int VPL, bool USE_LDS, int MODE, int NP>
 __global__ void __launch_bounds__(kQueryThreads)
-k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrs fp,
+k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrsT<NP> fp,
              long long Q, int N, int RS, int L, unsigned* __restrict__ sync,
              unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
              float* __restrict__ out) {
@@ -529,7 +534,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
     const float** ptab = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // [nf4][4]
-    int* woffs_all = reinterpret_cast<int*>(ptab + kFastPtrs);  // per wave: (64 / L) queries x nf4
+    int* woffs_all = reinterpret_cast<int*>(ptab + NP);  // per wave: (64 / L) queries x nf4
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
     const int lane = tid & (kWave - 1);
@@ -543,7 +548,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const long long i_end = q1 * L;
     CBN_STAMP(0);
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
-    if (tid < kFastPtrs) ptab[tid] = fp.p[tid];
+    if (tid < NP) ptab[tid] = fp.p[tid];
     (void)ns;
     CBN_STAMP(1);
     __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
@@ -809,6 +814,39 @@ __global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long lon
         out[i] = out[i] / m;
 }
 
+// k_scale over up to kScaleBatch (out, n) pairs in one launch (blockIdx.y =
+// pair b, dividing by the max of max_in[b * n_max, (b + 1) * n_max)): the
+// pipelined sharded stepper exchanges and scales several steps at once.
+constexpr int kScaleBatch = 8;
+struct ScaleBatch {
+    float* out[kScaleBatch];
+    long long n[kScaleBatch];
+};
+
+__global__ void __launch_bounds__(256) k_scale_batch(ScaleBatch sb, const unsigned* __restrict__ max_in, int n_max) {
+    const int b = blockIdx.y;
+    float* __restrict__ out = sb.out[b];
+    const long long n = sb.n[b];
+    const unsigned* mi = max_in + (long long)b * n_max;
+    unsigned mb = 0;
+    for (int i = threadIdx.x & (kWave - 1); i < n_max; i += kWave) mb = max(mb, mi[i]);
+    mb = wave_max_u(mb);
+    const float m = __uint_as_float(mb);
+    const long long n4 = n / 4;
+    float4* o4 = reinterpret_cast<float4*>(out);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 v = o4[i];
+        v.x = v.x / m;
+        v.y = v.y / m;
+        v.z = v.z / m;
+        v.w = v.w / m;
+        o4[i] = v;
+    }
+    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = out[i] / m;
+}
+
 // *out = max of n words (public query_max: per-block maxima -> one word)
 __global__ void __launch_bounds__(64) k_reduce_max(const unsigned* __restrict__ in, int n, unsigned* __restrict__ out) {
     unsigned m = 0;
@@ -845,18 +883,51 @@ int cbn::launch_scale(float* out, long long n, const unsigned* words, int n_word
 namespace {
 
 // this call's column pointer of every (factor, observed parent)
-FPtrs fast_ptrs(const cbn_plan* p, const EvPtrs& ev) {
-    FPtrs fp;
+template <int NP>
+FPtrsT<NP> fast_ptrs(const cbn_plan* p, const EvPtrs& ev) {
+    FPtrsT<NP> fp;
     // dummy for factors with no observed parent: any column of >= 1 row
     const float* dummy = p->ns > 0 ? ev.p[0] : p->d_image;
-    for (int i = 0; i < kFastPtrs; ++i) fp.p[i] = p->fast_slot[i] >= 0 ? ev.p[p->fast_slot[i]] : nullptr;
-    for (int f = 0; f < kFastPtrs / kFastObs; ++f) {
+    for (int i = 0; i < NP; ++i) fp.p[i] = p->fast_slot[i] >= 0 ? ev.p[p->fast_slot[i]] : nullptr;
+    for (int f = 0; f < NP / kFastObs; ++f) {
         uintptr_t v = reinterpret_cast<uintptr_t>(fp.p[f * kFastObs]);
         if (!v) v = reinterpret_cast<uintptr_t>(dummy) | kTagNone;
         if (fp.p[f * kFastObs + 1]) v |= kTagMore;
         fp.p[f * kFastObs] = reinterpret_cast<const float*>(v);
     }
     return fp;
+}
+
+// one fast-kernel launch with the pointer table sized to the plan
+template <int VPL, bool LDS, int MODE, int NP>
+void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
+                    unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
+    hipLaunchKernelGGL((k_query_fast<VPL, LDS, MODE, NP>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
+                       p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs<NP>(p, ev), Q, p->N, p->RS, L,
+                       p->d_sync, epoch, max_in, n_max, max_out, out);
+}
+
+template <int VPL, bool LDS, int MODE>
+void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
+                   unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
+    if (p->nf * kFastObs <= kFastPtrsSmall)
+        launch_fast_np<VPL, LDS, MODE, kFastPtrsSmall>(p, blocks, s, ev, Q, L, epoch, max_in, n_max, max_out, out);
+    else
+        launch_fast_np<VPL, LDS, MODE, kFastPtrs>(p, blocks, s, ev, Q, L, epoch, max_in, n_max, max_out, out);
+}
+
+template <int VPL, bool LDS, int MODE>
+const void* fast_kernel_fn(int nf) {
+    return nf * kFastObs <= kFastPtrsSmall ? reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>)
+                                           : reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>);
+}
+
+template <int VPL, bool LDS, int MODE>
+void allow_fast_lds(int bytes) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 // WRITE=false: per-block maxima -> max_out[0, max_slots); WRITE=true: divide by
@@ -869,10 +940,8 @@ int launch_fast_v(cbn_plan* p, long long Q, const EvPtrs& ev, const unsigned* ma
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
     if (!WRITE) n_max = p->max_slots;
-    hipLaunchKernelGGL((k_query_fast<VPL, LDS, WRITE ? kModeWrite : kModeMax>), dim3((unsigned)blocks),
-                       dim3(kQueryThreads), p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image,
-                       p->image_floats, fast_ptrs(p, ev), Q, p->N, p->RS, L, p->d_sync, 0u, max_in, n_max, max_out,
-                       out);
+    launch_fast_k<VPL, LDS, WRITE ? kModeWrite : kModeMax>(p, (unsigned)blocks, s, ev, Q, L, 0u, max_in, n_max,
+                                                          max_out, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -886,9 +955,7 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     const long long blocks = (Q + per_block - 1) / per_block;
     const unsigned epoch = ++p->fused_epoch;  // 1, 2, ... (0 = never published)
     if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
-    hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeFused>), dim3((unsigned)blocks), dim3(kQueryThreads),
-                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
-                       p->RS, L, p->d_sync, epoch, nullptr, 0, max_bits, out);
+    launch_fast_k<VPL, LDS, kModeFused>(p, (unsigned)blocks, s, ev, Q, L, epoch, nullptr, 0, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -899,9 +966,7 @@ int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits,
     const long long cap = p->max_slots;
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((k_query_fast<VPL, LDS, kModeRaw>), dim3((unsigned)blocks), dim3(kQueryThreads),
-                       p->fast_lds_bytes, s, p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs(p, ev), Q, p->N,
-                       p->RS, L, p->d_sync, 0u, nullptr, p->max_slots, max_bits, out);
+    launch_fast_k<VPL, LDS, kModeRaw>(p, (unsigned)blocks, s, ev, Q, L, 0u, nullptr, p->max_slots, max_bits, out);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -964,18 +1029,12 @@ void allow_lds(size_t bytes) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if constexpr (VEC == 4) {
         constexpr int M = WRITE ? kModeWrite : kModeMax;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, M>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, M>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, kModeFused>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeFused>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, LDS, kModeRaw>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, LDS, kModeRaw>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        allow_fast_lds<1, LDS, M>((int)bytes);
+        allow_fast_lds<2, LDS, M>((int)bytes);
+        allow_fast_lds<1, LDS, kModeFused>((int)bytes);
+        allow_fast_lds<2, LDS, kModeFused>((int)bytes);
+        allow_fast_lds<1, LDS, kModeRaw>((int)bytes);
+        allow_fast_lds<2, LDS, kModeRaw>((int)bytes);
     }
 }
 
@@ -1272,20 +1331,15 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             if (!getenv("CBN_NO_FUSED")) {
                 // the grid barrier needs every block resident: check one block per CU fits
                 // (tables in LDS, or -- image beyond LDS -- read from L2/HBM)
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<1, false, kModeFused>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<2, false, kModeFused>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+                allow_fast_lds<1, true, kModeFused>(kLdsBudget);
+                allow_fast_lds<2, true, kModeFused>(kLdsBudget);
+                allow_fast_lds<1, false, kModeFused>(kLdsBudget);
+                allow_fast_lds<2, false, kModeFused>(kLdsBudget);
                 int nb = 0;
-                const void* fn =
-                    P->use_lds ? (vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, true, kModeFused>)
-                                           : reinterpret_cast<const void*>(&k_query_fast<1, true, kModeFused>))
-                               : (vpl == 2 ? reinterpret_cast<const void*>(&k_query_fast<2, false, kModeFused>)
-                                           : reinterpret_cast<const void*>(&k_query_fast<1, false, kModeFused>));
+                const void* fn = P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors)
+                                                        : fast_kernel_fn<1, true, kModeFused>(n_factors))
+                                            : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors)
+                                                        : fast_kernel_fn<1, false, kModeFused>(n_factors));
                 if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, P->fast_lds_bytes) ==
                         hipSuccess && nb >= 1)
                     P->fused_ok = true;
@@ -1493,6 +1547,30 @@ int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, vo
     if (n == 0) return CBN_OK;
     if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_scale: out must be 16-B aligned");
     return launch_scale(out, (long long)n, max_bits, (int)n_max, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batches, const uint32_t* max_bits,
+                    int32_t n_max, void* stream) {
+    if (n_batches < 0 || n_batches > kScaleBatch || n_max < 1 || (n_batches > 0 && (!outs || !n_elems || !max_bits)))
+        return set_err(CBN_E_ARG, "cbn_scale_batch: bad arguments (at most %d batches)", kScaleBatch);
+    if (n_batches == 0) return CBN_OK;
+    ScaleBatch sb;
+    memset(&sb, 0, sizeof(sb));
+    long long most = 0;
+    for (int b = 0; b < n_batches; ++b) {
+        if (n_elems[b] < 0 || (n_elems[b] > 0 && !outs[b])) return set_err(CBN_E_ARG, "cbn_scale_batch: bad batch %d", b);
+        if (reinterpret_cast<uintptr_t>(outs[b]) % 16) return set_err(CBN_E_ARG, "cbn_scale_batch: out must be 16-B aligned");
+        sb.out[b] = outs[b];
+        sb.n[b] = n_elems[b];
+        most = std::max(most, (long long)n_elems[b]);
+    }
+    long long blocks = (most / 4 + 255) / 256;
+    const long long cap = std::max(1LL, 4LL * num_cu() / n_batches);
+    blocks = std::max(1LL, std::min(blocks, cap));
+    hipLaunchKernelGGL(k_scale_batch, dim3((unsigned)blocks, (unsigned)n_batches), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), sb, max_bits, (int)n_max);
+    HIP_TRY(hipGetLastError());
+    return CBN_OK;
 }
 
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms) {

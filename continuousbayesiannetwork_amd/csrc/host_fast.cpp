@@ -21,6 +21,9 @@
 
 #include <dlfcn.h>
 
+#include <array>
+#include <chrono>
+
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -92,6 +95,7 @@ py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots,
 }
 
 using scale_fn = int (*)(float*, int64_t, const unsigned*, int32_t, hipStream_t);
+using scale_batch_fn = int (*)(float* const*, const int64_t*, int32_t, const unsigned*, int32_t, hipStream_t);
 
 #define CBN_HIP_OK(x)                                                                   \
     do {                                                                                \
@@ -165,85 +169,149 @@ void nccl_comm_destroy(uintptr_t comm) {
 // ------------------------------------------------------- pipelined stepper --
 // distributed.ShardedStepper's per-step work in one host call (the Python
 // version -- events, stream switch, c10d all_reduce, record_stream -- cost
-// ~50 us of host time per step, 4x the GPU time of a 65k-query raw launch):
-//   compute stream A: raw launch -> words[slot]; ready event
-//   comm stream C:    wait ready; ncclAllReduce(MAX) of words[slot]; scale
-// Word slots form a ring of 2D; A waits for C only once every D steps (on the
-// event C recorded after step k-1, k % D == 0), which covers every slot the
-// next D steps overwrite (their previous users are steps <= k-1-D).  The rows
-// are recorded on C for the caching allocator.
+// ~50 us of host time per step, 4x the GPU time of a 65k-query raw launch).
+// Steps are exchanged in groups of G:
+//   compute stream A: raw launch of each step -> its words slot
+//   comm stream C:    after the group's G-th raw launch (ready event), ONE
+//                     ncclAllReduce(MAX) over the group's G x W words and ONE
+//                     cbn_scale_batch launch dividing each step's rows by its max
+// so the per-exchange host costs (event record + cross-stream wait ~5.5 us,
+// scale launch ~4.3 us, measured on MI355X by host_timing()) are paid once
+// per G steps.  Word slots form a ring of two groups; A waits for C only when
+// it starts a group whose slots the exchange two groups back still reads.
+// Rows are recorded on C for the caching allocator.  flush() (wait(),
+// synchronize()) exchanges a partial group.
 class Stepper {
   public:
-    Stepper(uintptr_t run_addr, uintptr_t scale_addr, uintptr_t plan, py::tuple slots, py::object first,
-            int64_t device_index, int64_t n_samples, bool target_observed, int64_t n_words, int depth,
+    Stepper(uintptr_t run_addr, uintptr_t scale_batch_addr, uintptr_t plan, py::tuple slots, py::object first,
+            int64_t device_index, int64_t n_samples, bool target_observed, int64_t n_words, int group,
             uintptr_t comm)
-        : run_(reinterpret_cast<run_fn>(run_addr)), scale_(reinterpret_cast<scale_fn>(scale_addr)),
+        : run_(reinterpret_cast<run_fn>(run_addr)), scale_batch_(reinterpret_cast<scale_batch_fn>(scale_batch_addr)),
           plan_(reinterpret_cast<void*>(plan)), slots_(slots), first_(first), dev_(device_index),
-          n_samples_(n_samples), target_observed_(target_observed), W_(n_words), D_(depth < 1 ? 1 : depth),
-          comm_(reinterpret_cast<ncclComm_t>(comm)),
+          n_samples_(n_samples), target_observed_(target_observed), W_(n_words),
+          G_(group < 1 ? 1 : (group > 8 ? 8 : group)), comm_(reinterpret_cast<ncclComm_t>(comm)),
           cs_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_index)) {
-        words_ = at::zeros({2 * D_, W_}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev_));
+        words_ = at::zeros({2 * G_, W_}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev_));
         CBN_HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-        CBN_HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+        for (auto& e : done_) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         CBN_HIP_OK(hipEventCreateWithFlags(&tail_, hipEventDisableTiming));
     }
     ~Stepper() {
         (void)hipEventDestroy(ready_);
-        (void)hipEventDestroy(done_);
+        for (auto e : done_) (void)hipEventDestroy(e);
         (void)hipEventDestroy(tail_);
     }
 
-    // rows (complete once the comm stream ran this step's scale), None when a
-    // fast check failed, or an int error code from the C ABI.
+    // rows (final once this step's group has been exchanged and scaled on the
+    // comm stream -- after wait()), None when a fast check failed, or an int
+    // error code from the C ABI.
     py::object step(py::dict evidence, py::object out_obj, int32_t flags) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         Cols c;
         if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return py::none();
         const hipStream_t A = c10::hip::getCurrentHIPStream(dev_).stream();
-        const hipStream_t C = cs_.stream();
-        if (k_ >= D_ && k_ % D_ == 0) CBN_HIP_OK(hipStreamWaitEvent(A, done_, 0));
+        const int half = (int)(g_ & 1);
+        if (pend_.empty() && used_[half]) CBN_HIP_OK(hipStreamWaitEvent(A, done_[half], 0));
         at::Tensor out = out_obj.is_none()
                              ? at::empty({c.n, n_samples_}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev_))
                              : THPVariable_Unpack(out_obj.ptr());
-        int* w = words_.data_ptr<int>() + (k_ % (2 * D_)) * W_;
+        int* w = words_.data_ptr<int>() + ((int64_t)half * G_ + (int64_t)pend_.size()) * W_;
+        const auto t1 = clk::now();
         int rc = run_(plan_, c.n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()), reinterpret_cast<unsigned*>(w),
                       static_cast<float*>(out.data_ptr()), flags, A);
         if (rc) return py::int_(rc);
-        CBN_HIP_OK(hipEventRecord(ready_, A));
-        CBN_HIP_OK(hipStreamWaitEvent(C, ready_, 0));
-        if (comm_) CBN_NCCL_OK(g_rccl.all_reduce(w, w, (size_t)W_, ncclInt32, ncclMax, comm_, C));
-        rc = scale_(static_cast<float*>(out.data_ptr()), out.numel(), reinterpret_cast<const unsigned*>(w),
-                    (int32_t)W_, C);
-        if (rc) return py::int_(rc);
+        const auto t2 = clk::now();
+        pend_.push_back(out);
         ++k_;
-        if (k_ % D_ == 0) CBN_HIP_OK(hipEventRecord(done_, C));
-        c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), cs_);
-        return py::cast(out);
+        if ((int)pend_.size() == G_) {
+            rc = flush_();
+            if (rc) return py::int_(rc);
+        }
+        py::object r = py::cast(out);
+        const auto t3 = clk::now();
+        tacc_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        tacc_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+        tacc_[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
+        ++tn_;
+        return r;
     }
 
-    // the current stream waits for every enqueued exchange + scale
+    // exchange + scale the pending partial group, then the current stream
+    // waits for every enqueued exchange
     void wait() {
+        check_(flush_());
         if (!k_) return;
         CBN_HIP_OK(hipEventRecord(tail_, cs_.stream()));
         CBN_HIP_OK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(dev_).stream(), tail_, 0));
     }
-    void synchronize() { CBN_HIP_OK(hipStreamSynchronize(cs_.stream())); }
+    void synchronize() {
+        check_(flush_());
+        CBN_HIP_OK(hipStreamSynchronize(cs_.stream()));
+    }
     uintptr_t comm_stream() const { return reinterpret_cast<uintptr_t>(cs_.stream()); }
     int64_t steps() const { return k_; }
+    int group() const { return G_; }
+
+    // mean host microseconds per step: gather + alloc, raw launch, the
+    // step's share of the group exchange (event, ncclAllReduce, scale) + return
+    std::vector<double> host_timing() {
+        std::vector<double> r(3, 0.0);
+        for (int i = 0; i < 3; ++i) r[i] = tn_ ? tacc_[i] / tn_ : 0.0;
+        tacc_.fill(0.0);
+        tn_ = 0;
+        return r;
+    }
 
   private:
+    int flush_() {
+        if (pend_.empty()) return 0;
+        const hipStream_t A = c10::hip::getCurrentHIPStream(dev_).stream();
+        const hipStream_t C = cs_.stream();
+        const int half = (int)(g_ & 1);
+        const int nb = (int)pend_.size();
+        int* w = words_.data_ptr<int>() + (int64_t)half * G_ * W_;
+        CBN_HIP_OK(hipEventRecord(ready_, A));
+        CBN_HIP_OK(hipStreamWaitEvent(C, ready_, 0));
+        if (comm_) CBN_NCCL_OK(g_rccl.all_reduce(w, w, (size_t)nb * W_, ncclInt32, ncclMax, comm_, C));
+        float* outs[8];
+        int64_t ns[8];
+        for (int b = 0; b < nb; ++b) {
+            outs[b] = static_cast<float*>(pend_[b].data_ptr());
+            ns[b] = pend_[b].numel();
+        }
+        const int rc = scale_batch_(outs, ns, nb, reinterpret_cast<const unsigned*>(w), (int32_t)W_, C);
+        if (rc) return rc;
+        CBN_HIP_OK(hipEventRecord(done_[half], C));
+        used_[half] = true;
+        for (auto& t : pend_) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), cs_);
+        pend_.clear();
+        ++g_;
+        return 0;
+    }
+    static void check_(int rc) {
+        if (rc) throw std::runtime_error("cbn_scale_batch failed (rc=" + std::to_string(rc) + ")");
+    }
+
     run_fn run_;
-    scale_fn scale_;
+    scale_batch_fn scale_batch_;
     void* plan_;
     py::tuple slots_;
     py::object first_;
     int64_t dev_, n_samples_;
     bool target_observed_;
-    int64_t W_, D_;
+    int64_t W_;
+    int G_;
     ncclComm_t comm_;
     c10::hip::HIPStream cs_;
     at::Tensor words_;
-    hipEvent_t ready_ = nullptr, done_ = nullptr, tail_ = nullptr;
-    int64_t k_ = 0;
+    std::vector<at::Tensor> pend_;
+    hipEvent_t ready_ = nullptr, tail_ = nullptr;
+    hipEvent_t done_[2] = {nullptr, nullptr};
+    bool used_[2] = {false, false};
+    int64_t k_ = 0, g_ = 0;
+    std::array<double, 3> tacc_{};
+    int64_t tn_ = 0;
 };
 
 // cbn_scale on the current stream of out's device (sharded path, after the
@@ -270,5 +338,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("wait", &Stepper::wait)
         .def("synchronize", &Stepper::synchronize)
         .def("comm_stream", &Stepper::comm_stream)
-        .def("steps", &Stepper::steps);
+        .def("steps", &Stepper::steps)
+        .def("group", &Stepper::group)
+        .def("host_timing", &Stepper::host_timing);
 }

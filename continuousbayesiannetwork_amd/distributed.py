@@ -105,31 +105,36 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
 
 class ShardedStepper:
     """Pipelined ``sharded_infer`` for a stream of query batches (serving /
-    the multi-GPU bench): step i's exchange overlaps step i+1's raw launch.
+    the multi-GPU bench): the exchange of a group of steps overlaps the next
+    steps' raw launches.
 
-    Per step, in ONE native host call (``_cbn_host.Stepper``): on the caller's
-    (compute) stream, ONE raw launch (unnormalised rows + per-block max words
-    into a ring slot) and an event; on the stepper's comm stream, wait for that
-    event, ``ncclAllReduce(MAX)`` of the words on our own RCCL communicator,
-    scale the rows in place, mark the slot free.  The compute stream waits for
-    the exchange only to reuse a ring slot ``depth`` steps later, so the RCCL
-    latency hides behind the next batch's launch.  (The same choreography in
-    Python -- events, stream switch, c10d all_reduce, record_stream -- cost
-    ~50 us of host time per step: tools/shard_step_probe.py.)
+    Per step, in ONE native host call (``_cbn_host.Stepper``), on the
+    caller's (compute) stream: ONE raw launch (unnormalised rows + per-block
+    max words into a ring slot).  Every ``exchange_every`` steps (G), on the
+    stepper's comm stream: wait for the group's last launch, ONE
+    ``ncclAllReduce(MAX)`` over the group's G x W words on our own RCCL
+    communicator, ONE ``cbn_scale_batch`` launch dividing each step's rows by
+    its own global max.  The per-exchange host costs (event + cross-stream
+    wait, scale launch: ~10 us on MI355X) are paid once per G steps and the
+    RCCL latency hides behind the next group's launches.  (The same
+    choreography in Python -- events, stream switch, c10d all_reduce,
+    record_stream -- cost ~50 us of host time per step:
+    tools/shard_step_probe.py.)
 
-    The returned rows are complete once the comm stream has run the step's
-    scale: call ``wait()`` (the current stream waits for the comm stream)
-    before reading them on another stream.  Results equal ``sharded_infer``
-    (and the single-process ``infer`` on the concatenated batch) bit for bit.
-    Every rank must call ``step`` the same number of times (one collective per
-    step).  Plans without a raw launch, and evidence the native checks reject,
-    fall back to the serial ``sharded_infer`` (c10d collectives).
+    A step's rows are final once its group has been exchanged: call
+    ``wait()`` (exchanges a partial group; the current stream then waits for
+    the comm stream) before reading them.  Results equal ``sharded_infer`` (and
+    the single-process ``infer`` on the concatenated batch) bit for bit.
+    Every rank calls ``step`` and ``wait`` the same number of times, in the
+    same order (the exchanges are collectives).  Plans without a raw launch,
+    and evidence the native checks reject, fall back to the serial
+    ``sharded_infer`` (c10d collectives) after flushing the pending group.
     """
 
-    def __init__(self, bn, target_node: str, N_max: int = 16, group=None, depth: int = 4,
+    def __init__(self, bn, target_node: str, N_max: int = 16, group=None, exchange_every: int = 4,
                  force_exchange: bool = False):
         self.bn, self.target, self.N_max, self.group = bn, target_node, N_max, group
-        self.depth = max(1, depth)
+        self.G = max(1, min(8, exchange_every))
         # force_exchange: all-reduce even at world size 1 (exercises RCCL on one GPU)
         self.exchange = force_exchange or (dist.is_initialized() and dist.get_world_size(group) > 1)
         self._c = None
@@ -137,6 +142,7 @@ class ShardedStepper:
         self._comm = 0
 
     def _setup(self, evidence_shard) -> bool:
+        import ctypes
         import os
 
         from . import _native
@@ -157,8 +163,9 @@ class ShardedStepper:
                 world, rank, uid = 1, 0, host.nccl_unique_id(rccl)
             self._comm = host.nccl_comm_init(rccl, uid, world, rank, fp.device.index)
         plan = fp.plan
-        self._c = host.Stepper(fp.run_fn, fp.scale_fn, plan.handle.value, fp.slot_keys, fp.first, fp.device.index,
-                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.depth, self._comm)
+        scale_batch = ctypes.cast(_native.load().cbn_scale_batch, ctypes.c_void_p).value
+        self._c = host.Stepper(fp.run_fn, scale_batch, plan.handle.value, fp.slot_keys, fp.first, fp.device.index,
+                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.G, self._comm)
         self._fp = fp
         return True
 

@@ -146,6 +146,12 @@ int32_t cbn_plan_max_words(const cbn_plan* plan);
  * `stream`): the global-max division of bayesian_network.py:296 after a
  * CBN_RUN_RAW launch and the cross-rank all-reduce of its words. */
 int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, void* stream);
+/* cbn_scale for up to 8 batches in one launch: outs[b][0, n_elems[b]) /=
+ * max over max_bits[b * n_max, (b + 1) * n_max) (outs / n_elems: host arrays
+ * of device pointers / sizes).  The pipelined sharded step exchanges and
+ * scales several raw launches at once (distributed.ShardedStepper). */
+int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batches, const uint32_t* max_bits,
+                    int32_t n_max, void* stream);
 int cbn_plan_status(cbn_plan* plan, int32_t* status);
 
 /* Average device time (ms) of the max and write passes over the timed calls

@@ -308,11 +308,12 @@ def test_raw_launch_sharded_equals_single_launch(Q, shards, gpu):
     np.testing.assert_array_equal(one.cpu().numpy(), full.cpu().numpy())
 
 
-@pytest.mark.parametrize("depth,exchange", [(1, False), (2, True), (4, False), (4, True)])
-def test_sharded_stepper_pipelined_equals_infer(depth, exchange, gpu):
-    """ShardedStepper (raw launch on the compute stream, exchange + scale on
-    its comm stream, ring of max-word buffers) over a stream of distinct
-    batches == infer on each batch, bit for bit -- including rows released
+@pytest.mark.parametrize("every,exchange", [(1, False), (2, True), (3, False), (4, True), (8, True)])
+def test_sharded_stepper_pipelined_equals_infer(every, exchange, gpu):
+    """ShardedStepper (raw launch on the compute stream; exchange + batched
+    scale of every ``every`` steps on its comm stream; ring of max-word slots)
+    over a stream of distinct batches (7 per pass: partial groups flushed by
+    wait()) == infer on each batch, bit for bit -- including rows released
     early (the allocator must not recycle them before the comm stream's scale)."""
     from continuousbayesiannetwork_amd.distributed import ShardedStepper
 
@@ -322,7 +323,7 @@ def test_sharded_stepper_pipelined_equals_infer(depth, exchange, gpu):
     batches = [_t(sample_evidence(data, cols, names, 4096 + 1000 * i, 30 + i), gpu) for i in range(7)]
     ref = [bn.infer("X19", b, N_max=32)[0].clone() for b in batches]
     # exchange: a one-rank RCCL communicator of the stepper's own (no process group)
-    st = ShardedStepper(bn, "X19", 32, depth=depth, force_exchange=exchange)
+    st = ShardedStepper(bn, "X19", 32, exchange_every=every, force_exchange=exchange)
     keep = []
     for rep in range(3):
         for i, b in enumerate(batches):

@@ -69,7 +69,15 @@ report("serial raw + all_reduce + scale", serial, 2000)
 st0 = ShardedStepper(bn, "X19", 32)
 report("pipelined ShardedStepper.step, no exchange", lambda: st0.step(ev), 2000)
 st0.close()
+st1 = ShardedStepper(bn, "X19", 32, exchange_every=1, force_exchange=True)
+report("pipelined ShardedStepper.step, exchange every step", lambda: st1.step(ev), 2000)
+st1.close()
 st = ShardedStepper(bn, "X19", 32, force_exchange=True)
 report("pipelined ShardedStepper.step", lambda: st.step(ev), 2000)
+flags = bn.engine.raw_flags(st._fp.plan)
+report("native Stepper.step called directly", lambda: st._c.step(ev, None, flags), 2000)
+if rank == 0:
+    names = ["gather+alloc", "raw launch", "exchange share + return"]
+    print("  native step phases (us):", {k: round(v, 2) for k, v in zip(names, st._c.host_timing())}, flush=True)
 st.close()
 dist.destroy_process_group()
