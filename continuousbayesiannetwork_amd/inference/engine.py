@@ -370,6 +370,8 @@ class InferenceEngine:
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
                       plan.n_samples, plan.target_observed, words.data_ptr(),
                       self._flags(plan) | _native.CBN_RUN_RAW, out)
+        if res is None:  # evidence the native checks reject (dtype, device, layout): convert, launch here
+            res = self._run_raw_converted(fp, evidence, words, out)
         if res is None or (type(res) is int and res == _native.CBN_E_UNSUPPORTED):
             return None
         if type(res) is int:
@@ -386,6 +388,23 @@ class InferenceEngine:
             return rows
 
         return res, tdom, words, scale
+
+    def _run_raw_converted(self, fp: "_FastPath", evidence, words: torch.Tensor, out):
+        """Raw launch with the evidence converted to contiguous float32 columns
+        on the plan's device (the reference's shape errors raise as in _run);
+        None when the batch has no rows or the target is unobserved with > 1."""
+        plan = fp.plan
+        n = next(iter(evidence.values())).shape[0]
+        if n == 0 or (not plan.target_observed and n != 1):
+            return None
+        cols = self._columns(plan, evidence, n, fp.device)
+        if out is None:
+            out = torch.empty((n, plan.n_samples), dtype=torch.float32, device=fp.device)
+        ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        with torch.cuda.device(fp.device):
+            rc = _native.load().cbn_plan_run(plan.handle, n, ptrs, len(cols), words.data_ptr(), _native.ptr(out),
+                                             self._flags(plan) | _native.CBN_RUN_RAW, _native.stream_ptr(fp.device))
+        return rc if rc else out  # (converted copies: stream-ordered frees on the launch stream)
 
     def raw_fast_path(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int) -> Optional["_FastPath"]:
         """The cached fast path of (target, evidence keys, N) when its plan takes
