@@ -1487,6 +1487,33 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
         if (e) HIP_TRY(hipEventRecord(e[2], s));
         return CBN_OK;
     }
+    if (plan->fast && n_queries > 0 && !(flags & CBN_RUN_TWO_PASS) && reinterpret_cast<uintptr_t>(out) % 16 == 0) {
+        // beyond the single launch: ONE compute pass (raw: unnormalised rows +
+        // per-block maxima) and an HBM-bound in-place scale that reduces the
+        // words, divides and publishes the max in *max_bits -- instead of
+        // computing every product twice (max pass + write pass)
+        if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
+        if (!max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+        EvPtrs ev;
+        memset(&ev, 0, sizeof(ev));
+        for (int i = 0; i < n_evidence; ++i) {
+            if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+            ev.p[i] = evidence[i];
+        }
+        unsigned* words = plan->d_sync + kMaxWordOff;
+        if (plan->use_lds)
+            rc = plan->vpl == 2 ? launch_raw_v<2, true>(plan, n_queries, ev, words, out, s)
+                                : launch_raw_v<1, true>(plan, n_queries, ev, words, out, s);
+        else
+            rc = plan->vpl == 2 ? launch_raw_v<2, false>(plan, n_queries, ev, words, out, s)
+                                : launch_raw_v<1, false>(plan, n_queries, ev, words, out, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[1], s));
+        rc = launch_scale(out, n_queries * (long long)plan->N, words, plan->max_slots, max_bits, s);
+        if (rc) return rc;
+        if (e) HIP_TRY(hipEventRecord(e[2], s));
+        return CBN_OK;
+    }
     if (plan->fast && n_queries > 0) {
         // two launches: per-block maxima into the plan's words, then the write
         // pass reduces them itself and publishes the max in *max_bits

@@ -6,7 +6,8 @@ profiles/ by hand).
 Per batch size: queries/s and effective GB/s (algorithmic bytes: 4 B per
 evidence value read + 4*N B per output row written) with HIP events around
 the timed loop on the launch stream.  Batches up to the fused capacity run as
-one launch; larger ones as two launches (max pass + write pass).
+one launch; larger ones as one raw compute pass + an in-place scale pass
+(``--two-pass``-style max + write launches are also timed for comparison).
 """
 import json
 import os
@@ -52,8 +53,13 @@ def main():
         k = max(5, min(200, (1 << 24) // q))
         t = timed(lambda: bn.infer("X19", ev, N_max=32), k)
         byt = q * (4 * len(names) + 4 * 32)
-        rows.append(dict(queries=q, launches=1 if q <= cap else 2, us_per_call=round(t * 1e6, 2),
-                         queries_per_s=round(q / t, 1), effective_GBps=round(byt / t / 1e9, 1)))
+        bn.engine.fused = False  # max pass + write pass (both compute every product)
+        bn.infer("X19", ev, N_max=32)
+        t2 = timed(lambda: bn.infer("X19", ev, N_max=32), k)
+        bn.engine.fused = True
+        rows.append(dict(queries=q, path="fused" if q <= cap else "raw + scale", us_per_call=round(t * 1e6, 2),
+                         queries_per_s=round(q / t, 1), effective_GBps=round(byt / t / 1e9, 1),
+                         two_pass_us=round(t2 * 1e6, 2)))
         print(rows[-1], flush=True)
         del ev
     # PCIe-inclusive: evidence in pinned host memory -> device, marginals -> pinned host
