@@ -121,6 +121,17 @@ CASES = [
          ev=[], Q=1, N=3, evidence_none=True, expect_error=True),
     dict(name="err_target_parent_free", data=("chain", 5, 4, 500, 12), target="X4",
          ev=["X1"], Q=8, N=4, expect_error=True),
+    # BASELINE configs[1] shape (the headline network) at a reference-friendly batch
+    dict(name="chain20_d32_config1", data=("chain_stay", 20, 32, 20000, 21, 0.8), target="X19",
+         ev=[f"X{i}" for i in range(19)], Q=256, N=32, ev_seed=201),
+    # configs[2] shape: alarm-like 37-node DAG, in-degree <= 4, d = 8 (tests/helpers.py)
+    dict(name="alarm37_d8_config2", data=("alarm", 20000, 22), target="X36",
+         ev=[f"X{i}" for i in range(36)], Q=96, N=8, ev_seed=202),
+    dict(name="alarm37_d8_partial", data=("alarm", 20000, 23), target="X35",
+         ev=[f"X{i}" for i in range(0, 35, 2)], Q=12, N=8, ev_seed=203),
+    # configs[4] shape at a size where the 25-factor product stays finite: 5 x 5 grid, d = 4
+    dict(name="grid5_d4_config4", data=("grid", 20000, 24, 5, 4), target="X24",
+         ev=[f"X{i}" for i in range(24)], Q=64, N=4, ev_seed=204),
 ]
 
 
@@ -128,6 +139,16 @@ def make_data(spec):
     if spec[0] == "chain":
         vals = spec[5] if len(spec) > 5 else None
         return chain_data(spec[1], spec[2], spec[3], spec[4], vals)
+    if spec[0] in ("alarm", "grid", "chain_stay"):
+        sys.path.insert(0, os.path.dirname(HERE))
+        from helpers import alarm_like_data, grid_data
+        from helpers import chain_data as chain_stay
+
+        if spec[0] == "chain_stay":  # bench.py's generator: X_i = X_{i-1} w.p. stay, else uniform
+            return chain_stay(spec[1], spec[2], spec[3], spec[4], stay=spec[5])
+        if spec[0] == "alarm":
+            return alarm_like_data(spec[1], spec[2])
+        return grid_data(spec[1], spec[2], side=spec[3], d=spec[4], keep=0.9)
     return multi_data(spec[1], spec[2])
 
 
@@ -137,8 +158,12 @@ def main():
     import torch
 
     BayesianNetwork = _load_reference()
+    only = set(sys.argv[1:])  # regenerate just these cases (default: all)
     manifest = []
     for c in CASES:
+        if only and c["name"] not in only:
+            manifest.append(c["name"])
+            continue
         data, cols, edges = make_data(c["data"])
         dag = nx.DiGraph()
         dag.add_nodes_from(cols)
@@ -146,7 +171,7 @@ def main():
         df = pd.DataFrame(data, columns=cols)
         bn = BayesianNetwork(dag, df, {"estimator_name": "brute_force"},
                              {"inference_obj": "exact"}, device="cpu")
-        ev = sample_evidence(data, cols, c["ev"], c["Q"], seed=100 + len(manifest),
+        ev = sample_evidence(data, cols, c["ev"], c["Q"], seed=c.get("ev_seed", 100 + len(manifest)),
                              missing_frac=c.get("missing", 0.0))
         ev_t = {k: torch.tensor(v) for k, v in ev.items()}
         if c.get("evidence_none"):
