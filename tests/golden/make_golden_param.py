@@ -121,6 +121,12 @@ CASES = [
          ev=["C", "D"], Q=32, N=5),
     dict(name="logreg_multi_partial", est="logistic_regression", data=("multi", 400, 30), target="C",
          ev=["A"], Q=20, N=4, seed=3),
+    # BASELINE configs[3] shape: 50-node mixed continuous / 20-level discrete DAG
+    # (tests/helpers.mixed_dag_data, unit-scaled), evidence on the 49 non-target nodes
+    dict(name="lr_mixed50_config3", est="linear_regression", data=("mixed50", 2000, 41), target="X49",
+         ev=[f"X{i}" for i in range(49)], Q=32, N=16),
+    dict(name="nn_mixed50_config3", est="neural_network", data=("mixed50", 2000, 42), target="X49",
+         ev=[f"X{i}" for i in range(49)], Q=32, N=16, model={"hidden_dims": [16], "activation": "tanh"}),
 ]
 
 
@@ -129,6 +135,11 @@ def make_data(spec, unit=False):
     LogisticRegression estimators train a BCE-with-logits loss, whose logits
     diverge on targets outside [0, 1] until exp(-(x - mu)) overflows and the
     reference's density turns NaN (kept as one edge case)."""
+    if spec[0] == "mixed50":
+        sys.path.insert(0, os.path.dirname(HERE))
+        from helpers import mixed_dag_data
+
+        return mixed_dag_data(spec[1], spec[2], n=50, unit=True)
     data, cols, edges = chain_cont(spec[1], spec[2], spec[3]) if spec[0] == "chain" else mixed_multi(spec[1], spec[2])
     if unit:
         lo, hi = data.min(0), data.max(0)
@@ -156,8 +167,12 @@ def main():
     import torch
 
     BayesianNetwork = _load_reference()
+    only = set(sys.argv[1:])  # regenerate just these cases (default: all)
     manifest = []
     for i, c in enumerate(CASES):
+        if only and c["name"] not in only:
+            manifest.append(c["name"])
+            continue
         torch.manual_seed(1000 + i)
         data, cols, edges = make_data(c["data"], c.get("unit", False))
         dag = nx.DiGraph()
