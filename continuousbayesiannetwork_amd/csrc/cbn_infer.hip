@@ -661,6 +661,38 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (wbase + nthr < i_end) load_x(wbase + nthr, 0);
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        if constexpr (!USE_LDS) {
+            // tables in L2 / MALL (image beyond LDS): KB factors' row loads in
+            // flight before their products (memory-level parallelism for the
+            // gather), multiplied in factor order
+            constexpr int KB = VPL == 2 ? 6 : 8;  // 48 / 32 VGPRs of rows in flight (8 at VPL 2 spills)
+            for (int f0 = 0; f0 < nf; f0 += KB) {
+                int oo[KB];
+#pragma unroll
+                for (int k = 0; k < KB; ++k) oo[k] = f0 + k < nf ? my[f0 + k] : -1;
+                float4 t[KB][VPL];
+#pragma unroll
+                for (int k = 0; k < KB; ++k) {
+                    const int o = oo[k];
+                    const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v)
+                        t[k][v] = (f0 + k < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int k = 0; k < KB; ++k) {
+                    if (f0 + k < nf) {
+#pragma unroll
+                        for (int v = 0; v < VPL; ++v) {
+                            acc[4 * v + 0] = acc[4 * v + 0] * t[k][v].x;
+                            acc[4 * v + 1] = acc[4 * v + 1] * t[k][v].y;
+                            acc[4 * v + 2] = acc[4 * v + 2] * t[k][v].z;
+                            acc[4 * v + 3] = acc[4 * v + 3] * t[k][v].w;
+                        }
+                    }
+                }
+            }
+        } else
         for (int f0 = 0; f0 < nf; f0 += 4) {
             const int4 o4 = *reinterpret_cast<const int4*>(my + f0);
             const int oo[4] = {o4.x, o4.y, o4.z, o4.w};
