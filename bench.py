@@ -198,25 +198,26 @@ def main():
         ntimed, twrite_ms = K, ev0.elapsed_time(ev1) / K
     if ntimed:
         tmax, twrite = tmax_ms * 1e-3, twrite_ms * 1e-3
-        n_cols = len(names)  # evidence columns read by the write pass
-        bytes_write = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
-        achieved = bytes_write / twrite / 1e9
+        n_cols = len(names)  # evidence columns read per query
+        bytes_q = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
         vpl = int(os.environ.get("CBN_FAST_VPL", "2"))
         nptr = 128 if 4 * n <= 128 else 416  # kernel-argument pointer table sized to the plan (n factors)
-        kname = f"k_query_fast<{vpl}, true, {2 if fused else 1}, {nptr}>"  # <VPL, LDS, MODE 2 fused / 1 write, NP>
+        # the dominant kernel: fused single launch; beyond its capacity the raw
+        # compute pass (then an HBM-bound scale); --two-pass: the write pass
+        mode, what, t_dom = ((2, "single launch: both passes", twrite) if fused else
+                             (1, "write pass", twrite) if a.two_pass else (3, "raw compute pass", tmax))
+        kname = f"k_query_fast<{vpl}, true, {mode}, {nptr}>"  # <VPL, LDS, MODE, NP>
+        achieved = bytes_q / t_dom / 1e9
         traffic, tsrc = pmc_traffic(kname)
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                        kernel=kname + (" (single launch: both passes)" if fused else " (write pass)"),
-                        avg_us=round(twrite * 1e6, 2), algorithmic_bytes_per_launch=bytes_write,
-                        timed_steps=ntimed)
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel=f"{kname} ({what})",
+                        avg_us=round(t_dom * 1e6, 2), algorithmic_bytes_per_launch=bytes_q, timed_steps=ntimed)
         if tsrc:
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
         roofline["timing"] = ("HIP events on the launch stream around the whole timed region / K launches" if fused
-                              else "HIP events around the write pass of every 8th step (library-side)")
-
+                              else "HIP events around the launches of every 8th step (library-side)")
         if not fused:
-            roofline["max_pass_us"] = round(tmax * 1e6, 2)
+            roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
 
     cold = None
     if not sharded and not a.rebuild_tables:
