@@ -218,6 +218,20 @@ def main():
                               else "HIP events around the launches of every 8th step (library-side)")
         if not fused:
             roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
+    elif sharded:
+        # sharded step (raw launch + all-reduce(max) of the block words + in-place
+        # scale, overlapped across steps): per-GPU algorithmic bytes of one step =
+        # evidence in + raw rows out + the scale's read and write of the rows,
+        # over this rank's HIP-event step time on the launch stream
+        n_cols = len(names)
+        bytes_step = Q * (4 * n_cols + 3 * 4 * d)
+        t_step = ev0.elapsed_time(ev1) / K * 1e-3
+        achieved = bytes_step / t_step / 1e9
+        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                        kernel="sharded step: k_query_fast raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
+                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_step, timed_steps=K,
+                        timing="HIP events on rank 0's launch stream around the timed region / K steps")
 
     cold = None
     if not sharded and not a.rebuild_tables:
