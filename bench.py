@@ -86,6 +86,8 @@ def parse():
                     help="run the N>1 step (raw launch + RCCL all-reduce + scale, pipelined) even at N=1")
     ap.add_argument("--serial-exchange", action="store_true",
                     help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
+    ap.add_argument("--exchange-every", type=int, default=8,
+                    help="N>1: steps per all-reduce + scale group (1..8)")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
@@ -144,9 +146,10 @@ def main():
     it = [0]
     # N>1: one raw launch per step on the compute stream; the all-reduce(MAX)
     # of the block max words + the in-place scale run on a comm stream, once per
-    # 4 steps for all 4, so the exchange overlaps the next steps' launches
+    # --exchange-every steps (8) for all of them, so the exchange overlaps the next steps' launches
     # (distributed.ShardedStepper)
-    stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else 4, force_exchange=sharded)
+    stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
+                             force_exchange=sharded)
 
     def step():
         ev = batches[it[0] % len(batches)]
