@@ -149,10 +149,11 @@ def alarm_like_data(S, seed, n=37, d=8, max_parents=4, n_edges=46):
     return X.astype(np.float32), cols, edges
 
 
-def grid_data(S, seed, side=10, d=64, keep=0.8):
+def grid_data(S, seed, side=10, d=64, keep=0.8, noise=2):
     """BASELINE configs[4]-shaped network: side x side grid DAG (node (r, c)
     has parents (r, c-1) and (r-1, c)), d levels per node: X = mean of the
-    parents + small noise (mod d) with probability ``keep``, else uniform."""
+    parents + small noise (mod d, |noise| <= ``noise``) with probability
+    ``keep``, else uniform."""
     rng = np.random.default_rng(seed)
     n = side * side
     X = np.zeros((S, n), np.int64)
@@ -167,5 +168,5 @@ def grid_data(S, seed, side=10, d=64, keep=0.8):
                 continue
             base = sum(X[:, p] for p in ps) // len(ps)
             k = rng.random(S) < keep
-            X[:, i] = np.where(k, (base + rng.integers(-2, 3, S)) % d, rng.integers(0, d, S))
+            X[:, i] = np.where(k, (base + rng.integers(-noise, noise + 1, S)) % d, rng.integers(0, d, S))
     return X.astype(np.float32), [f"X{i}" for i in range(n)], edges
