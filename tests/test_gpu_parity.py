@@ -448,6 +448,33 @@ def test_grid_beyond_64_factors_and_evidence_columns(gpu):
         assert part.shape[0] == 150
 
 
+def test_grid_full_config4_shape_matches_oracle_fixture(gpu):
+    """The full configs[4] plan (10 x 10 grid, d = N = 64, 100 factors, 99
+    evidence columns, 85 MB global-table image) with peaked CPDs whose fp32
+    products stay finite, vs the oracle's marginals committed by
+    tests/golden/make_grid_oracle.py (data + evidence regenerated from the same
+    seeds); the raw launch + scale path (sharded_infer, no process group)
+    == the single call bit for bit."""
+    import os
+
+    from continuousbayesiannetwork_amd.distributed import sharded_infer
+
+    from helpers import grid_data
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "grid10_d64_peaked_oracle.npz"))
+    data, cols, edges = grid_data(60000, 3, side=10, d=64, keep=0.995, noise=0)
+    target, names = cols[-1], cols[:-1]
+    ev = _t(sample_evidence(data, cols, names, 64, 5), gpu)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    pdf, dom = bn.infer(target, ev, N_max=64)
+    np.testing.assert_array_equal(dom.cpu().numpy(), z["domain"])
+    out = pdf.cpu().numpy()
+    assert np.isfinite(out).all()
+    np.testing.assert_allclose(out, z["pdf"], rtol=RTOL, atol=ATOL)
+    one, _ = sharded_infer(bn, target, ev, N_max=64)
+    np.testing.assert_array_equal(one.cpu().numpy(), out)
+
+
 def test_grid_fast_path_beyond_64_factors(gpu):
     """9 x 9 grid, d = N = 32 (4 lanes per query): the fast table kernel with
     81 factors and 80 evidence columns -- single launch == two launches ==
