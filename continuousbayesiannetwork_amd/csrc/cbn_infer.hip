@@ -156,15 +156,23 @@ __device__ __forceinline__ unsigned wave_max_u(unsigned v) {
 // kernels' phases into a debug buffer (never read by the kernels themselves).
 #ifdef CBN_STAMPS
 __device__ unsigned long long* g_stamps = nullptr;
+// the buffer pointer is read ONCE per wave (CBN_STAMP_INIT, after stamp 0's
+// clock read); a stamp is then one s_memrealtime + one un-waited store
+#define CBN_STAMP_INIT                                                                        \
+    const unsigned long long _t0 = __builtin_amdgcn_s_memrealtime();                          \
+    unsigned long long* const _stp = g_stamps;                                                \
+    if (_stp && (threadIdx.x & 63) == 0)                                                      \
+        _stp[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12] = _t0
 #define CBN_STAMP(k)                                                                          \
     do {                                                                                      \
         __builtin_amdgcn_sched_barrier(0);                                                    \
         unsigned long long _t = __builtin_amdgcn_s_memrealtime(); /* 100 MHz, chip-wide */   \
-        if (g_stamps && (threadIdx.x & 63) == 0)                                              \
-            g_stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12 + (k)] = _t; \
+        if (_stp && (threadIdx.x & 63) == 0)                                                  \
+            _stp[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12 + (k)] = _t; \
         __builtin_amdgcn_sched_barrier(0);                                                    \
     } while (0)
 #else
+#define CBN_STAMP_INIT do {} while (0)
 #define CBN_STAMP(k) do {} while (0)
 #endif
 
@@ -187,15 +195,26 @@ __device__ __forceinline__ float gload(const float* p, long long i) {
     return ((gfloat_t*)p)[i];
 }
 typedef const __attribute__((address_space(1))) void gbl_void_t;
+typedef const __attribute__((address_space(4))) int cint_t;
+
+// Four ints through the constant address space: at a wave-uniform address that
+// is one s_load_dwordx4 (a generic load issued after LDS-DMA or other writes
+// would be a vector load: the compiler cannot prove the memory unclobbered).
+__device__ __forceinline__ int4 sload_int4(const void* p) {
+    const cint_t* q = reinterpret_cast<const cint_t*>(reinterpret_cast<uintptr_t>(p));
+    return make_int4(q[0], q[1], q[2], q[3]);
+}
 
 // Copy n4 float4 from global to LDS with LDS-DMA (global_load_lds_dwordx4: no
 // VGPR staging; one wave-instruction moves 1 KiB).  Chunk order is rotated by
 // block so the CUs do not all hit the same L2 channel at once.  Completion is
 // awaited by the caller's __syncthreads() (it waits vmcnt(0)).
-__device__ __forceinline__ void lds_dma_copy(const float* __restrict__ g, float4* lds, int n4) {
+__device__ __forceinline__ void lds_dma_copy(const float* __restrict__ g, float4* lds, int n4,
+                                             int nw = kQueryThreads / kWave) {
+    // nw: waves per block (a compile-time default: reading blockDim costs a
+    // kernel-argument line fetch on the launch's critical path)
     const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    const int nw = blockDim.x / kWave;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int nchunk = (n4 + kWave - 1) / kWave;
     for (int c0 = wave; c0 < nchunk; c0 += nw) {
         const int c = (c0 + (int)blockIdx.x) % nchunk;
@@ -524,12 +543,60 @@ constexpr int kLoc = 8;
 constexpr int kModeMax = 0, kModeWrite = 1, kModeFused = 2, kModeRaw = 3;
 constexpr unsigned kSpinLimit = 1u << 22;  // bounded barrier spin (~0.3 s): never hang
 
+// Fused grid barrier on the global max, called by ONE wave per block (all
+// blocks co-resident).  Slot barrier: no counters, no re-arming.  One relaxed
+// agent-scope 8-byte store publishes {epoch, block max} (single-copy atomic, so
+// a reader sees the old epoch or the new pair, never a mix); the wave then
+// polls every block's slot (lane i owns slots i, i+64, ...) until all carry
+// this epoch -- one round trip after the last block arrives instead of a chain
+// of fan-in atomics.  Returns the max word of all blocks.  Bounded spin: a
+// block that never arrives sets sync[2] (the timeout flag) instead of hanging.
+__device__ __forceinline__ unsigned slot_barrier_max(unsigned* __restrict__ sync, unsigned epoch, float bm) {
+    const int lane = threadIdx.x & (kWave - 1);
+    unsigned long long* slots = reinterpret_cast<unsigned long long*>(sync + kSlotWordOff);
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    if (lane == 0)
+        __hip_atomic_store(&slots[blockIdx.x], tag | __float_as_uint(bm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int G = gridDim.x;
+    constexpr int kPer = kMaxSlots / kWave;
+    unsigned gm = 0;
+    unsigned spins = 0;
+    for (;;) {
+        // all of this round's loads in flight before any is consumed (a
+        // per-slot branch would serialise them: one round trip each)
+        unsigned long long v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+            if (k * kWave < G)  // wave-uniform
+                v[k] = __hip_atomic_load(&slots[min(lane + k * kWave, G - 1)], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        bool done = true;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (k * kWave < G) {
+                const bool here = (v[k] >> 32) == (unsigned long long)epoch;
+                done &= here;
+                const unsigned b = here ? (unsigned)v[k] : 0u;
+                gm = gm > b ? gm : b;
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kSpinLimit) {
+            if (lane == 0) atomicOr(&sync[2], 1u);
+            break;
+        }
+    }
+    return wave_max_u(gm);  // non-negative floats: unsigned order == float order
+}
+
 template <int VPL, bool USE_LDS, int MODE, int NP>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrsT<NP> fp,
-             long long Q, int N, int RS, int L, unsigned* __restrict__ sync,
+             long long Q, long long per, int N, int RS, int L, int paired, unsigned* __restrict__ sync,
              unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
              float* __restrict__ out) {
+    CBN_STAMP_INIT;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
@@ -542,11 +609,11 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const int qpw = kWave / L;  // queries per wave per round
     int* woffs = woffs_all + wid * qpw * nf4;
     float* wmax = reinterpret_cast<float*>(woffs_all + (nthr / kWave) * qpw * nf4);
-    const long long per = (Q + gridDim.x - 1) / gridDim.x;
+    // per = ceil(Q / gridDim.x), from the host (a 64-bit division here is ~150
+    // scalar instructions on the launch's critical path)
     const long long q0 = (long long)blockIdx.x * per;
     const long long q1 = q0 + per < Q ? q0 + per : Q;
     const long long i_end = q1 * L;
-    CBN_STAMP(0);
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
     if (tid < NP) ptab[tid] = fp.p[tid];
     (void)ns;
@@ -570,6 +637,19 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const int qi = lane / L;  // query slot of this lane within the wave
     const int l = lane - qi * L;
     int* my = woffs + qi * nf4;
+    // Paired layout (VPL 2, L 4, N 32): ds_read_b128 serves a wave in four
+    // 16-lane groups, each holding four queries with distinct qi & 3.  Slot g =
+    // qi & 3 reads the odd factor of each pair first (g >= 2) and the upper
+    // half of each row first (g odd), so the four queries of a group always read
+    // four different 16-bank quarters (bank half = factor parity).  The lane's
+    // outputs: cols [clo, clo + 4) in acc[0..3], [chi, chi + 4) in acc[4..7].
+    const bool pr = VPL == 2 && USE_LDS && paired;
+    const int g4 = qi & 3;
+    const bool swp = pr && (g4 >> 1) != 0;
+    const int h0 = pr ? (g4 & 1) : 0;
+    int col[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) col[v] = pr ? (l + 4 * (v ^ h0)) * 4 : (l * VPL + v) * 4;
     bool first = true;
     constexpr int NV = 4 * VPL;  // outputs owned by this lane
     float acc[NV];
@@ -692,6 +772,43 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                     }
                 }
             }
+        } else if (pr) {
+            // factor pairs (f, f + 1) in bank halves 0 / 1: four reads per pair,
+            // the multiplies in the reference's factor order whatever the read order
+            constexpr int H = 4 % NV;  // acc[H..H+3]: the lane's second column block (VPL 2)
+            for (int f0 = 0; f0 < nf; f0 += 4) {
+                const int4 o4 = *reinterpret_cast<const int4*>(my + f0);
+                const int oo[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+                for (int k = 0; k < 4; k += 2) {
+                    if (f0 + k + 1 < nf) {
+                        const int o1 = swp ? oo[k + 1] : oo[k], o2 = swp ? oo[k] : oo[k + 1];
+                        const float* b1 = img + (o1 < 0 ? 0 : o1);
+                        const float* b2 = img + (o2 < 0 ? 0 : o2);
+                        float4 r0 = *reinterpret_cast<const float4*>(b1 + col[0]);
+                        float4 r1 = *reinterpret_cast<const float4*>(b1 + col[VPL - 1]);
+                        float4 r2 = *reinterpret_cast<const float4*>(b2 + col[0]);
+                        float4 r3 = *reinterpret_cast<const float4*>(b2 + col[VPL - 1]);
+                        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (o1 < 0) r0 = r1 = z;
+                        if (o2 < 0) r2 = r3 = z;
+                        const float4 a0 = swp ? r2 : r0, a1 = swp ? r3 : r1;
+                        const float4 c0 = swp ? r0 : r2, c1 = swp ? r1 : r3;
+                        acc[0] *= a0.x; acc[1] *= a0.y; acc[2] *= a0.z; acc[3] *= a0.w;
+                        acc[H + 0] *= a1.x; acc[H + 1] *= a1.y; acc[H + 2] *= a1.z; acc[H + 3] *= a1.w;
+                        acc[0] *= c0.x; acc[1] *= c0.y; acc[2] *= c0.z; acc[3] *= c0.w;
+                        acc[H + 0] *= c1.x; acc[H + 1] *= c1.y; acc[H + 2] *= c1.z; acc[H + 3] *= c1.w;
+                    } else if (f0 + k < nf) {  // odd factor count: the last one alone
+                        const int o = oo[k];
+                        const float* b = img + (o < 0 ? 0 : o);
+                        float4 r0 = *reinterpret_cast<const float4*>(b + col[0]);
+                        float4 r1 = *reinterpret_cast<const float4*>(b + col[VPL - 1]);
+                        if (o < 0) r0 = r1 = make_float4(0.f, 0.f, 0.f, 0.f);
+                        acc[0] *= r0.x; acc[1] *= r0.y; acc[2] *= r0.z; acc[3] *= r0.w;
+                        acc[H + 0] *= r1.x; acc[H + 1] *= r1.y; acc[H + 2] *= r1.z; acc[H + 3] *= r1.w;
+                    }
+                }
+            }
         } else
         for (int f0 = 0; f0 < nf; f0 += 4) {
             const int4 o4 = *reinterpret_cast<const int4*>(my + f0);
@@ -719,16 +836,17 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (valid && CBN_OK_OR(q < Q && (long long)(l + 1) * VPL * 4 <= N, 3)) {
             if (MODE == kModeFused) fq = q;
             if (MODE == kModeWrite) {
-                float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
+                float* o = out + q * N;
 #pragma unroll
                 for (int v = 0; v < VPL; ++v)
-                    o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
-                                       acc[4 * v + 3] / maxv);
+                    *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                        acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
             } else if (MODE == kModeRaw) {
-                float4* o = reinterpret_cast<float4*>(out + q * N) + l * VPL;
+                float* o = out + q * N;
 #pragma unroll
                 for (int v = 0; v < VPL; ++v)
-                    o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+                    *reinterpret_cast<float4*>(o + col[v]) =
+                        make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
 #pragma unroll
                 for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
             } else {
@@ -758,50 +876,8 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (lane == 0) wmax[wid] = lmax;
         __syncthreads();
         if (wid == 0) {
-            // Slot barrier: no counters, no re-arming.  One relaxed agent-scope
-            // 8-byte store publishes {epoch, block max} (single-copy atomic, so a
-            // reader sees the old epoch or the new pair, never a mix); wave 0 of
-            // every block then polls the slots it has not yet seen (lane i owns
-            // slots i, i+64, ...) until all G carry this epoch -- one round trip
-            // after the last block arrives instead of a chain of fan-in atomics.
             const int nw = nthr / kWave;
-            const float bm = wave_max(lane < nw ? wmax[lane] : 0.f);
-            unsigned long long* slots = reinterpret_cast<unsigned long long*>(sync + kSlotWordOff);
-            const unsigned long long tag = (unsigned long long)epoch << 32;
-            if (lane == 0)
-                __hip_atomic_store(&slots[blockIdx.x], tag | __float_as_uint(bm), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            const int G = gridDim.x;
-            constexpr int kPer = kMaxSlots / kWave;
-            unsigned gm = 0;
-            unsigned spins = 0;
-            for (;;) {
-                // all of this round's loads in flight before any is consumed (a
-                // per-slot branch would serialise them: one round trip each)
-                unsigned long long v[kPer];
-#pragma unroll
-                for (int k = 0; k < kPer; ++k)
-                    if (k * kWave < G)  // wave-uniform
-                        v[k] = __hip_atomic_load(&slots[min(lane + k * kWave, G - 1)], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-                bool done = true;
-#pragma unroll
-                for (int k = 0; k < kPer; ++k) {
-                    if (k * kWave < G) {
-                        const bool here = (v[k] >> 32) == (unsigned long long)epoch;
-                        done &= here;
-                        const unsigned b = here ? (unsigned)v[k] : 0u;
-                        gm = gm > b ? gm : b;
-                    }
-                }
-                if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > kSpinLimit) {  // a block never arrived: flag it, do not hang
-                    if (lane == 0) atomicOr(&sync[2], 1u);
-                    break;
-                }
-            }
-            gm = wave_max_u(gm);  // non-negative floats: unsigned order == float order
+            const unsigned gm = slot_barrier_max(sync, epoch, wave_max(lane < nw ? wmax[lane] : 0.f));
             if (lane == 0) {
                 wmax[0] = __uint_as_float(gm);
                 if (blockIdx.x == 0 && max_out) *max_out = gm;
@@ -812,11 +888,298 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         CBN_STAMP(9);
         maxv = wmax[0];
         if (fq >= 0) {
-            float4* o = reinterpret_cast<float4*>(out + fq * N) + l * VPL;
+            float* o = out + fq * N;
 #pragma unroll
             for (int v = 0; v < VPL; ++v)
-                o[v] = make_float4(acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv,
-                                   acc[4 * v + 3] / maxv);
+                *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                    acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
+        }
+        CBN_STAMP(10);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Staged fast kernel: the paired N = 32 layout in LDS (four lanes per query,
+// eight columns per lane, <= 32 factors), all four modes.  A block walks its
+// query range in rounds of kSR = 256 queries (16 waves x 16 queries).
+//
+// Why a second kernel: k_query_fast's prologue is a serial chain per wave --
+// kernel arguments -> LDS-DMA of the image + pointer table -> block barrier ->
+// pointer reads -> evidence loads -> domain index (records read from LDS) ->
+// products; phase stamps put 6 us of a 15 us launch before the first product.
+// Here the evidence of a round is STAGED BY FACTOR: unit u = (factor f, 128
+// queries) belongs to wave u % 16, whose factor is wave-uniform, so its column
+// pointer and record come in on the scalar path, its loads are coalesced
+// 256-B requests, and the domain index + table offset is computed right
+// there; the offsets go to LDS ([query][slot], int2-readable).  The evidence
+// loads are issued BEFORE the image's LDS-DMA, so both latencies overlap, and
+// ONE block barrier covers both.
+//
+// Products (conflict-free, no selects): a factor f's rows live in bank half
+// f & 1 (the paired layout).  The four queries of a ds_read_b128 lane group
+// have distinct slot g = qi & 3; queries with g >= 2 ("lagged") run ONE FACTOR
+// BEHIND: their offset slot j holds factor j - 1 (slot 0: a ones row), the
+// others' slot j holds factor j.  Step t reads slots 2t and 2t + 1: at each
+// read the lagged queries are in the other bank half, and the row half read
+// first (g odd: the upper one) splits each half again -- four disjoint
+// 16-bank quarters per group -- while every lane still multiplies in the
+// reference's factor order.  A value outside a factor's domain points at a
+// zero row, slots past the last factor at a ones row (x * 1 is exact), so the
+// loop has no per-factor guards.
+constexpr int kSR = 256;  // queries per block round
+constexpr int kSQ = 128;  // queries per staging unit (two per lane)
+constexpr int kSU = 4;    // staging units per wave per round (nf <= 32 -> nf * 2 / 16 <= 4)
+
+template <int MODE>
+__global__ void __launch_bounds__(kQueryThreads)
+k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, int nf, int zero_off, long long Q,
+               long long per, unsigned* __restrict__ sync, unsigned epoch, const unsigned* __restrict__ max_in,
+               int n_max, unsigned* __restrict__ max_out, float* __restrict__ out, FPtrsT<kFastPtrsSmall> fp) {
+    CBN_STAMP_INIT;
+    constexpr int N = 32;
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float* simg = reinterpret_cast<float*>(smem4);
+    const int T = (nf + 2) >> 1;  // steps: slots 0 .. 2T-1 cover factors 0 .. nf-1 for both orders
+    const int nsl = 2 * T;        // offset slots per query
+    int* offs = reinterpret_cast<int*>(simg + image_floats);  // [2][kSR][nsl]
+    float* wmax = reinterpret_cast<float*>(offs + 2 * kSR * nsl);
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    // wave-uniform for the compiler too: the unit / factor indices derived from
+    // it then stay on the scalar path (s_load of pointers and records)
+    const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const long long q0 = (long long)blockIdx.x * per;
+    const long long q1 = q0 + per < Q ? q0 + per : Q;
+    const int nunits = nf * (kSR / kSQ);
+    const FastRec* grec = reinterpret_cast<const FastRec*>(gimage + rec_off);
+    const int one_off = zero_off + 64;  // ones super-row (zero super-row at zero_off)
+
+    // evidence of round `qr` for this wave's units -> x (first observed parent
+    // of each unit's factor), all loads in flight at once.  The column pointers
+    // (argument block) are wave-uniform scalar loads, all issued before the
+    // first is used.  Tags: kTagNone (no observed parent: a dummy column, row
+    // 0), kTagMore (further parents, rare: loaded in stage_store).
+    float x[kSU][2];
+    auto stage_load = [&](long long qr) {
+        uintptr_t pk[kSU];
+#pragma unroll
+        for (int k = 0; k < kSU; ++k) {
+            const int u = wid + k * (kQueryThreads / kWave);
+            pk[k] = reinterpret_cast<uintptr_t>(fp.p[(u < nunits ? u / (kSR / kSQ) : 0) * kFastObs]);
+        }
+#pragma unroll
+        for (int k = 0; k < kSU; ++k) {
+            const int u = wid + k * (kQueryThreads / kWave);
+            if (u < nunits) {  // wave-uniform
+                const float* col = reinterpret_cast<const float*>(pk[k] & ~(kTagMore | kTagNone));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const long long q = qr + (u % (kSR / kSQ)) * kSQ + h * kWave + lane;
+                    x[k][h] = gload(col, (pk[k] & kTagNone) ? 0 : (q < q1 ? q : q0));
+                }
+            }
+        }
+    };
+    // x -> domain index -> table offset (a value outside the fitted domain: the
+    // zero row of the factor's bank half) -> offs[buf][query][slot]; non-dense
+    // domains binary-search the sorted domain in the image's L2 copy (the LDS
+    // copy may not have landed yet)
+    auto stage_store = [&](long long qr, int buf) {
+        int* ob = offs + buf * kSR * nsl;
+        int4 rk[kSU];  // {table_off, n_obs, card[0], card[1]} of each unit's factor: all loads issued first
+#pragma unroll
+        for (int k = 0; k < kSU; ++k) {
+            const int u = wid + k * (kQueryThreads / kWave);
+            rk[k] = sload_int4(grec + (u < nunits ? u / (kSR / kSQ) : 0));
+        }
+#pragma unroll
+        for (int k = 0; k < kSU; ++k) {
+            const int u = wid + k * (kQueryThreads / kWave);
+            if (u < nunits) {
+                const int f = u / (kSR / kSQ);
+                const int n_obs = rk[k].y, c0 = rk[k].z;
+                const int zoff = zero_off + (f & 1) * 32;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int ql = (u % (kSR / kSQ)) * kSQ + h * kWave + lane;
+                    int o;
+                    if (n_obs == 1 && (c0 & kDenseBit)) {  // common case: one parent, domain {0..card-1}
+                        const int card = c0 & (kDenseBit - 1);
+                        const float xv = x[k][h];
+                        const int i = (int)xv;
+                        o = (xv >= 0.f && xv < (float)card && (float)i == xv) ? rk[k].x + i * 64 : zoff;
+                    } else if (n_obs == 0) {
+                        o = rk[k].x;
+                    } else {
+                        const FastRec& r = grec[f];
+                        float xs[kFastObs];
+                        xs[0] = x[k][h];
+                        if (n_obs > 1) {  // wave-uniform, rare
+                            const long long q = qr + ql;
+#pragma unroll
+                            for (int p = 1; p < kFastObs; ++p)
+                                if (p < n_obs) xs[p] = gload(fp.p[f * kFastObs + p], q < q1 ? q : q0);
+                        }
+                        int row = 0;
+                        bool ok = true;
+#pragma unroll
+                        for (int p = 0; p < kFastObs; ++p) {
+                            if (p < n_obs) {
+                                const int card = r.card[p] & (kDenseBit - 1);
+                                const float xv = xs[p];
+                                int i;
+                                if (r.card[p] & kDenseBit) {
+                                    i = (int)xv;
+                                    i = (xv >= 0.f && xv < (float)card && (float)i == xv) ? i : -1;
+                                } else {
+                                    i = bsearch_eq(gimage + r.dom_off[p], card, xv);
+                                }
+                                ok &= i >= 0;
+                                row = row * card + (i < 0 ? 0 : i);
+                            }
+                        }
+                        o = ok ? r.table_off + row * 64 : zoff;
+                    }
+                    // lagged queries ((ql & 2) != 0: slot g = qi & 3 >= 2) hold factor f in slot f + 1
+                    ob[ql * nsl + f + ((ql >> 1) & 1)] = o;
+                }
+            }
+        }
+    };
+
+    // padding slots (constant for the launch, both buffers): slot 0 of a lagged
+    // query and every slot past its last factor point at the ones row of the
+    // slot's bank half (slot j of a query with lag d holds factor j - d)
+    if (tid < kSR) {
+        const int d = (tid >> 1) & 1;
+        for (int j = 0; j < nsl; ++j) {
+            const int f = j - d;
+            if (f < 0 || f >= nf) {
+                const int o = one_off + (f & 1) * 32;
+                offs[tid * nsl + j] = o;
+                offs[kSR * nsl + tid * nsl + j] = o;
+            }
+        }
+    }
+    // evidence loads first, then the image's LDS-DMA: both latencies overlap
+    // (a wave's vector-memory counter drains in issue order, so loads issued
+    // after the DMA could not be consumed before it lands)
+    long long qr = q0;
+    if (qr < q1) stage_load(qr);
+    lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + zero/ones rows + domains + records
+    CBN_STAMP(1);
+    if (qr < q1) stage_store(qr, 0);
+    CBN_STAMP(2);
+    __syncthreads();  // image landed (vmcnt(0) of the DMA) + round 0 offsets
+    CBN_STAMP(3);
+
+    const int qi = lane >> 2;  // query slot in the wave (16 per wave)
+    const int l = lane & 3;
+    const int h0 = qi & 1;     // g odd: the row's upper half first
+    const int clo = (l + 4 * h0) * 4, chi = (l + 4 * (h0 ^ 1)) * 4;  // this lane's columns
+    float lmax = 0.f;
+    float maxv = 1.f;
+    if (MODE == kModeWrite) {
+        unsigned m = 0;
+        for (int i = lane; i < n_max; i += kWave) m = max(m, max_in[i]);
+        m = wave_max_u(m);
+        maxv = __uint_as_float(m);
+        if (max_out && blockIdx.x == 0 && tid == 0) *max_out = m;
+    }
+    float acc[8];
+    long long fq = -1;
+    int buf = 0;
+    for (; qr < q1; qr += kSR, buf ^= 1) {  // block-uniform
+        const long long qn = qr + kSR;
+        // next round's evidence flies during these products (the fused launch has one round)
+        if (MODE != kModeFused && qn < q1) stage_load(qn);
+        const int ql = wid * 16 + qi;
+        const long long q = qr + ql;
+        const int* my = offs + buf * kSR * nsl + ql * nsl;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        // step t: slots 2t, 2t + 1 -> four row reads (16 B each: this lane's two
+        // column blocks of two rows); step t + 1's reads are in flight while
+        // step t is multiplied
+        auto load_step = [&](int t, float4& r0, float4& r1, float4& r2, float4& r3) {
+            const int2 o = *reinterpret_cast<const int2*>(my + 2 * t);
+            r0 = *reinterpret_cast<const float4*>(simg + o.x + clo);
+            r1 = *reinterpret_cast<const float4*>(simg + o.x + chi);
+            r2 = *reinterpret_cast<const float4*>(simg + o.y + clo);
+            r3 = *reinterpret_cast<const float4*>(simg + o.y + chi);
+        };
+        auto mul_step = [&](const float4& r0, const float4& r1, const float4& r2, const float4& r3) {
+            acc[0] *= r0.x; acc[1] *= r0.y; acc[2] *= r0.z; acc[3] *= r0.w;
+            acc[4] *= r1.x; acc[5] *= r1.y; acc[6] *= r1.z; acc[7] *= r1.w;
+            acc[0] *= r2.x; acc[1] *= r2.y; acc[2] *= r2.z; acc[3] *= r2.w;
+            acc[4] *= r3.x; acc[5] *= r3.y; acc[6] *= r3.z; acc[7] *= r3.w;
+        };
+        float4 a0, a1, a2, a3, b0, b1, b2, b3;
+        load_step(0, a0, a1, a2, a3);
+        CBN_STAMP(4);
+        int t = 0;
+        for (; t + 2 <= T; t += 2) {
+            load_step(t + 1, b0, b1, b2, b3);
+            mul_step(a0, a1, a2, a3);
+            if (t + 2 < T) load_step(t + 2, a0, a1, a2, a3);
+            mul_step(b0, b1, b2, b3);
+        }
+        if (t < T) mul_step(a0, a1, a2, a3);
+        CBN_STAMP(5);
+        if (q < q1) {
+            if (MODE == kModeFused) fq = q;
+            if (MODE == kModeWrite || MODE == kModeRaw) {
+                const float dv = MODE == kModeWrite ? maxv : 1.f;
+                float* o = out + q * N;
+                *reinterpret_cast<float4*>(o + clo) = MODE == kModeWrite
+                    ? make_float4(acc[0] / dv, acc[1] / dv, acc[2] / dv, acc[3] / dv)
+                    : make_float4(acc[0], acc[1], acc[2], acc[3]);
+                *reinterpret_cast<float4*>(o + chi) = MODE == kModeWrite
+                    ? make_float4(acc[4] / dv, acc[5] / dv, acc[6] / dv, acc[7] / dv)
+                    : make_float4(acc[4], acc[5], acc[6], acc[7]);
+            }
+            if (MODE != kModeWrite)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) lmax = fmaxf(lmax, acc[i]);
+        }
+        if (MODE != kModeFused && qn < q1) {
+            stage_store(qn, buf ^ 1);
+            __syncthreads();  // next round's offsets visible; this round's buffer free
+        }
+    }
+    CBN_STAMP(6);
+    if (MODE == kModeMax || MODE == kModeRaw) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int i = 0; i < kQueryThreads / kWave; ++i) m = fmaxf(m, wmax[i]);
+            max_out[blockIdx.x] = __float_as_uint(m);  // one word per block, plain store
+        }
+        if (blockIdx.x == 0)  // words of blocks this launch does not have
+            for (int i = (int)gridDim.x + tid; i < n_max; i += kQueryThreads) max_out[i] = 0u;
+    }
+    if (MODE == kModeFused) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        CBN_STAMP(7);
+        if (wid == 0) {
+            const unsigned gm = slot_barrier_max(sync, epoch, wave_max(lane < kQueryThreads / kWave ? wmax[lane] : 0.f));
+            if (lane == 0) {
+                wmax[0] = __uint_as_float(gm);
+                if (blockIdx.x == 0 && max_out) *max_out = gm;
+            }
+        }
+        CBN_STAMP(8);
+        __syncthreads();
+        CBN_STAMP(9);
+        maxv = wmax[0];
+        if (fq >= 0) {
+            float* o = out + fq * N;
+            *reinterpret_cast<float4*>(o + clo) = make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
+            *reinterpret_cast<float4*>(o + chi) = make_float4(acc[4] / maxv, acc[5] / maxv, acc[6] / maxv, acc[7] / maxv);
         }
         CBN_STAMP(10);
     }
@@ -935,13 +1298,21 @@ template <int VPL, bool LDS, int MODE, int NP>
 void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
                     unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, MODE, NP>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
-                       p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs<NP>(p, ev), Q, p->N, p->RS, L,
-                       p->d_sync, epoch, max_in, n_max, max_out, out);
+                       p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs<NP>(p, ev), Q,
+                       (Q + blocks - 1) / blocks, p->N, p->RS, L, p->paired ? 1 : 0, p->d_sync, epoch, max_in, n_max,
+                       max_out, out);
 }
 
 template <int VPL, bool LDS, int MODE>
 void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
                    unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
+    if (p->staged) {  // paired N = 32 layout in LDS: the staged kernel (same grid, same words)
+        hipLaunchKernelGGL((k_query_staged<MODE>), dim3(blocks), dim3(kQueryThreads), p->staged_lds_bytes, s,
+                           p->d_image, p->image_floats, p->rec_off, p->nf, p->zero_off, Q, (Q + blocks - 1) / blocks,
+                           p->d_sync,
+                           epoch, max_in, n_max, max_out, out, fast_ptrs<kFastPtrsSmall>(p, ev));
+        return;
+    }
     if (p->nf * kFastObs <= kFastPtrsSmall)
         launch_fast_np<VPL, LDS, MODE, kFastPtrsSmall>(p, blocks, s, ev, Q, L, epoch, max_in, n_max, max_out, out);
     else
@@ -1166,8 +1537,28 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         total_rows += rows;
     }
     const bool global_tables = vec == 4 && total_rows * (N + 4) * 4 > (long long)kLdsBudget;
-    const int RS = vec == 4 && !global_tables ? N + 4 : N;
+    // Paired layout (N = 32, tables in LDS, 8 columns per lane): factor f's rows
+    // sit in bank half (f & 1) of 256-B super-rows -- even factors in banks 0-31,
+    // odd factors in banks 32-63, each class packed from super-row 0.  The fast
+    // kernel then reads the two factors of a pair (and the two halves of a row)
+    // in an order that gives the four queries of every ds_read_b128 lane group
+    // four disjoint 16-bank quarters: conflict-free row gathers (the padded
+    // layout's random rows collide ~2x, profiles/r02_lds_pmc.txt).
+    long long class_rows[2] = {0, 0};
+    int want_vpl = 2;
+    if (const char* e = getenv("CBN_FAST_VPL")) want_vpl = atoi(e);
+    for (int f = 0; f < n_factors; ++f) {
+        long long rows = 1;
+        for (int p = 0; p < factors[f].n_parents && p < kMaxP; ++p)
+            if (factors[f].parent_ev_slot[p] >= 0 && factors[f].parent_card[p] > 0)
+                rows = std::min(rows * factors[f].parent_card[p], 1LL << 40);
+        class_rows[f & 1] += rows;
+    }
+    const bool paired = vec == 4 && N == 32 && !global_tables && want_vpl >= 2 && !getenv("CBN_NO_PAIRED") &&
+                        std::max(class_rows[0], class_rows[1]) * 64 * 4 <= (long long)kLdsBudget * 3 / 4;
+    const int RS = paired ? 64 : vec == 4 && !global_tables ? N + 4 : N;
     const long long talign = global_tables ? 32 : 4;
+    long long class_start[2] = {0, 0};
     std::vector<DevFactor> fac(n_factors);
     std::vector<const float*> slot_dom(CBN_MAX_EVIDENCE, nullptr);
     std::vector<int> slot_card(CBN_MAX_EVIDENCE, 0);
@@ -1226,11 +1617,21 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         d.n_entries = (int)(rows * N);
         const long long F_eff = h.kind == CBN_FACTOR_SCALAR ? N : F;
         d.wave_mode = F_eff >= kWave ? 1 : 0;
-        d.table_off = (int)off;
-        off += (rows * RS + talign - 1) & ~(talign - 1);
+        if (paired) {
+            d.table_off = (int)(class_start[f & 1] * 64 + (f & 1) * 32);
+            class_start[f & 1] += rows;
+            off = std::max(class_start[0], class_start[1]) * 64;
+        } else {
+            d.table_off = (int)off;
+            off += (rows * RS + talign - 1) & ~(talign - 1);
+        }
     }
     for (int sl = 0; sl < ns; ++sl)
         if (!slot_dom[sl]) return set_err(CBN_E_ARG, "evidence slot %d is not used by any factor", sl);
+    // paired layout: a zero super-row (values outside a domain) and a ones
+    // super-row (padding slots) after the tables, both bank halves each
+    const long long zero_off = paired ? off : -1;
+    if (paired) off += 128;
     const long long table_floats = off;
     std::vector<QSlot> qs(ns);
     std::vector<float> hdom;
@@ -1257,6 +1658,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->L = L;
     P->image_floats = (int)off;
     P->table_floats = (int)table_floats;
+    P->zero_off = (int)zero_off;
     P->rec_off = (int)rec_off;
     P->RS = RS;
     // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
@@ -1301,6 +1703,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     ok = ok && (build.empty() ||
                 hipMemcpy(P->d_build, build.data(), sizeof(BuildItem) * build.size(), hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && hipMemset(P->d_image, 0, sizeof(float) * std::max<long long>(off, 4)) == hipSuccess;
+    if (ok && paired) {
+        const std::vector<float> ones(64, 1.f);
+        ok = hipMemcpy(P->d_image + zero_off + 64, ones.data(), sizeof(float) * 64, hipMemcpyHostToDevice) == hipSuccess;
+    }
     ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
     for (int sl = 0; ok && sl < ns; ++sl)
         ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
@@ -1352,6 +1758,18 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         if (fast) {
             P->fast = true;
             P->vpl = vpl;
+            P->paired = paired && vpl == 2 && P->use_lds;
+            const size_t st_bytes = img_bytes + (size_t)2 * kSR * (n_factors + 2) * 4 + (kQueryThreads / kWave) * 4 + 64;
+            if (P->paired && n_factors * kFastObs <= kFastPtrsSmall && st_bytes <= (size_t)kLdsBudget &&
+                !getenv("CBN_NO_STAGED")) {
+                P->staged = true;
+                P->staged_lds_bytes = (st_bytes + 15) & ~size_t(15);
+                for (const void* fn : {reinterpret_cast<const void*>(&k_query_staged<kModeMax>),
+                                       reinterpret_cast<const void*>(&k_query_staged<kModeWrite>),
+                                       reinterpret_cast<const void*>(&k_query_staged<kModeFused>),
+                                       reinterpret_cast<const void*>(&k_query_staged<kModeRaw>)})
+                    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
+            }
             P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
             P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
@@ -1368,12 +1786,13 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 allow_fast_lds<1, false, kModeFused>(kLdsBudget);
                 allow_fast_lds<2, false, kModeFused>(kLdsBudget);
                 int nb = 0;
-                const void* fn = P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors)
-                                                        : fast_kernel_fn<1, true, kModeFused>(n_factors))
-                                            : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors)
-                                                        : fast_kernel_fn<1, false, kModeFused>(n_factors));
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, P->fast_lds_bytes) ==
-                        hipSuccess && nb >= 1)
+                const void* fn = P->staged ? reinterpret_cast<const void*>(&k_query_staged<kModeFused>)
+                                 : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors)
+                                                          : fast_kernel_fn<1, true, kModeFused>(n_factors))
+                                              : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors)
+                                                          : fast_kernel_fn<1, false, kModeFused>(n_factors));
+                const size_t lb = P->staged ? P->staged_lds_bytes : P->fast_lds_bytes;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, lb) == hipSuccess && nb >= 1)
                     P->fused_ok = true;
             }
         }

@@ -72,6 +72,10 @@ struct cbn_plan {
     int rec_off = 0;             // float offset of the FastRec array in the image
     int RS = 1;                  // table row stride in floats (>= N; padded to spread LDS banks)
     int vpl = 1;                 // fast path: float4 chunks of one query row per lane
+    bool paired = false;         // N = 32 bank-half layout (RS = 64, factor f in half f & 1), VPL 2 in LDS
+    bool staged = false;         // paired plans of <= 32 factors: k_query_staged (evidence staged by factor)
+    size_t staged_lds_bytes = 0;
+    int zero_off = -1;           // paired layout: float offset of the zero super-row (ones super-row at +64)
     unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;

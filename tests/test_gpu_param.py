@@ -212,12 +212,42 @@ def test_parametric_raw_sharded_equals_single_call(Q, shards, gpu):
     np.testing.assert_array_equal(one.cpu().numpy(), full.cpu().numpy())
 
 
+@pytest.mark.parametrize("name", ["lr_mixed50_config3_full", "nn_mixed50_config3_full"])
+def test_config3_full_share_matches_reference(name, gpu, tmp_path):
+    """BASELINE configs[3] at one GPU's share of the 1 M-query batch (131 072
+    queries, 50-node mixed DAG, LinearRegression / NeuralNetwork [16] tanh, the
+    reference fixtures' fitted parameters): a 4 097-row slice (every 32nd row +
+    the batch argmax row) of the reference's output over the WHOLE batch,
+    normalised by its max (tests/golden/make_golden_full_param.py), at rtol 1e-5."""
+    import hashlib
+    import json
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    g = load_param_golden(meta["base"])
+    m = g["meta"]
+    bn = _fixture_bn(g, gpu, tmp_path)
+    names = [c for c in m["columns"] if c != m["target"]]
+    ev = sample_evidence(g["data"], m["columns"], names, meta["Q"], meta["ev_seed"])
+    h = hashlib.sha256()
+    for k in sorted(ev):
+        h.update(np.ascontiguousarray(ev[k]).tobytes())
+    assert h.hexdigest() == meta["evidence_sha256"]
+    random.seed(0)
+    pdf, dom = bn.infer(m["target"], _t(ev, gpu), N_max=m["N_max"])
+    p = pdf.cpu().numpy()
+    np.testing.assert_array_equal(dom.cpu().numpy(), z["domain"])
+    assert float(p[meta["argmax_row"]].max()) == 1.0 and float(np.nanmax(p)) == 1.0
+    np.testing.assert_allclose(p[z["rows"]], z["pdf"], rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("est,model", [("linear_regression", None),
                                        ("neural_network", {"hidden_dims": [16], "activation": "tanh"})])
 def test_config3_full_size_properties(est, model, gpu):
     """configs[3] shape at one GPU's share of the batch (50 nodes, 131 072
-    queries, evidence on the 49 non-target nodes): max exactly 1, duplicated
-    evidence rows identical, a sample of rows proportional to the oracle's."""
+    queries, evidence on the 49 non-target nodes, GPU-trained parameters): max
+    exactly 1, duplicated evidence rows identical, a sample of rows plus the
+    batch argmax row matches the oracle on the same parameters at rtol 1e-5."""
     # unit-scaled columns: with raw 0..19 levels and the reference's fixed
     # sigma = 1 (log_sigma is not in its optimizer, linear_regression.py:53),
     # the 50-factor product underflows to 0 in every column and 0 / 0 = NaN
@@ -235,10 +265,11 @@ def test_config3_full_size_properties(est, model, gpu):
     assert (p > 0).mean() > 0.99
     np.testing.assert_array_equal(p[0], p[1])
     ora = _oracle_from_bn(bn, edges, cols, data, est, (model or {}).get("activation"))
-    sub = np.arange(0, Q, Q // 61)[:60]
+    rstar = int(np.argmax(p.max(1)))
+    sub = np.append(np.arange(0, Q, Q // 61)[:60], rstar)  # + the argmax row: one normaliser for both
     ref, _ = ora.infer(cols[-1], {k: v[sub] for k, v in ev.items()}, 16)
-    scale = p[sub].max() / ref.max()
-    np.testing.assert_allclose(p[sub], ref * scale, rtol=2e-5, atol=1e-7)
+    assert ref[-1].max() == 1.0
+    np.testing.assert_allclose(p[sub], ref, rtol=RTOL, atol=ATOL)
 
 
 def _set_linear(est, W, b, log_scale, gpu):

@@ -54,3 +54,34 @@ def test_oracle_parametric_matches_reference_golden(name):
     assert pdf.shape == g["pdf"].shape
     np.testing.assert_array_equal(dom, g["domain"])
     np.testing.assert_allclose(pdf, g["pdf"], rtol=RTOL, atol=ATOL)
+
+
+def _full(name):
+    import json
+    import os
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"), allow_pickle=False)
+    return z["rows"], z["pdf"], z["domain"], json.loads(str(z["meta"]))
+
+
+@pytest.mark.parametrize("name,gen", [("chain20_d32_bench65536", "chain"), ("alarm37_d8_bench262144", "alarm")])
+def test_oracle_matches_full_batch_golden(name, gen):
+    """The full-batch reference goldens (tests/golden/make_golden_full.py): the
+    oracle on a few rows plus the batch argmax row (so it normalises by the same
+    max as the reference's whole-batch call) reproduces those rows."""
+    from helpers import alarm_like_data, chain_data, sample_evidence
+
+    rows, ref, rdom, m = _full(name)
+    if gen == "chain":
+        data, cols, edges = chain_data(20, 32, 200_000, 3, stay=0.8)
+    else:
+        data, cols, edges = alarm_like_data(200_000, 5)
+    ev = sample_evidence(data, cols, [c for c in cols if c != m["target"]], m["Q"], m["ev_seed"])
+    pick = np.array([0, 1, 2, 3, 5, 8, 13, 21, int(np.searchsorted(rows, m["argmax_row"]))])
+    sub = rows[pick]
+    bn = OracleBN(edges, cols, data)
+    pdf, dom = bn.infer(m["target"], {k: v[sub] for k, v in ev.items()}, m["N_max"])
+    assert (rdom == rdom[:1]).all()  # one sample domain per query row
+    np.testing.assert_array_equal(dom, np.broadcast_to(rdom[:1], dom.shape))
+    assert pdf[-1].max() == 1.0
+    np.testing.assert_allclose(pdf, ref[pick], rtol=RTOL, atol=ATOL)

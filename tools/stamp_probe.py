@@ -31,7 +31,7 @@ torch.cuda.synchronize()
 st = buf.view(-1, S).cpu().numpy()
 st = st[st[:, 0] > 0]
 print("waves stamped:", len(st), "fused" if bn.engine.fused else "two-pass (write pass stamps)")
-names = ["entry", "fill issued + sev", "sync (fill landed)", "ev loads issued", "offsets + wave exchange",
+names = ["entry", "kernargs + fill issued + ptab", "sync (fill landed)", "ev loads issued", "offsets + wave exchange",
          "products", "store/acc", "loop end", "barrier passed (tid0)", "block sync after barrier", "stored"]
 for k in range(1, 11):
     ok = (st[:, k] > 0) & (st[:, k - 1] > 0)
@@ -53,3 +53,5 @@ print("block arrival at barrier:        p50 %d p90 %d max %d" % tuple(np.percent
 print("per-block entry->arrival:        p50 %d p90 %d max %d" % tuple(np.percentile(a - e, [50, 90, 100])))
 late = np.argsort(e)[-8:]
 print("latest-entering blocks:", late.tolist(), (e[late] - t0).tolist())
+grp = np.array([e[b::8].min() - t0 for b in range(8)])
+print("first block entry per b % 8 group:", grp.tolist())
