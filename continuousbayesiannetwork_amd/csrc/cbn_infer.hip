@@ -197,6 +197,20 @@ __device__ __forceinline__ float gload(const float* p, long long i) {
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 typedef const __attribute__((address_space(4))) int cint_t;
 
+// Output rows are stored WRITE-THROUGH (sc1: the line leaves the XCD's L2 at
+// once instead of staying dirty): a launch that ends with 8 MB of plain stores
+// makes the next dependent launch wait for their write-back (the price
+// table's "boundary" row: + bytes / 6 TB/s).  rsrc = a buffer descriptor over
+// this block's rows (wave-uniform base and size), off = byte offset in it.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+    u32x4_t x = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);  // aux 16 = sc1
+}
+
 // Four ints through the constant address space: at a wave-uniform address that
 // is one s_load_dwordx4 (a generic load issued after LDS-DMA or other writes
 // would be a vector load: the compiler cannot prove the memory unclobbered).
@@ -959,13 +973,15 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // (argument block) are wave-uniform scalar loads, all issued before the
     // first is used.  Tags: kTagNone (no observed parent: a dummy column, row
     // 0), kTagMore (further parents, rare: loaded in stage_store).
-    float x[kSU][2];
+    float x[kSU][2] = {};
     auto stage_load = [&](long long qr) {
+        // (unconditional: u / 2 < 32 stays inside the table whatever nf is, so
+        // these scalar loads do not wait for the scalar arguments)
         uintptr_t pk[kSU];
 #pragma unroll
         for (int k = 0; k < kSU; ++k) {
             const int u = wid + k * (kQueryThreads / kWave);
-            pk[k] = reinterpret_cast<uintptr_t>(fp.p[(u < nunits ? u / (kSR / kSQ) : 0) * kFastObs]);
+            pk[k] = reinterpret_cast<uintptr_t>(fp.p[(u / (kSR / kSQ)) * kFastObs]);
         }
 #pragma unroll
         for (int k = 0; k < kSU; ++k) {
@@ -1065,10 +1081,14 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // (a wave's vector-memory counter drains in issue order, so loads issued
     // after the DMA could not be consumed before it lands)
     long long qr = q0;
+#ifndef CBN_ABL_NOSTAGE
     if (qr < q1) stage_load(qr);
+#endif
+#ifndef CBN_ABL_NODMA
     lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + zero/ones rows + domains + records
+#endif
     CBN_STAMP(1);
-    if (qr < q1) stage_store(qr, 0);
+    if (qr < q1) stage_store(qr, 0);  // (CBN_ABL_NOSTAGE: x uninitialised, offsets still in range)
     CBN_STAMP(2);
     __syncthreads();  // image landed (vmcnt(0) of the DMA) + round 0 offsets
     CBN_STAMP(3);
@@ -1089,6 +1109,8 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     float acc[8];
     long long fq = -1;
     int buf = 0;
+    const __amdgpu_buffer_rsrc_t orsrc =
+        rows_rsrc(MODE != kModeFused ? nullptr : out + q0 * N, MODE != kModeFused ? 0 : (q1 - q0) * (long long)(N * 4));
     for (; qr < q1; qr += kSR, buf ^= 1) {  // block-uniform
         const long long qn = qr + kSR;
         // next round's evidence flies during these products (the fused launch has one round)
@@ -1101,8 +1123,14 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         // step t: slots 2t, 2t + 1 -> four row reads (16 B each: this lane's two
         // column blocks of two rows); step t + 1's reads are in flight while
         // step t is multiplied
+        // all of the query's offsets first (slot pairs, <= 17 steps), so no row
+        // read waits on an offset read
+        int2 ov[17];
+#pragma unroll
+        for (int j = 0; j < 17; ++j)
+            if (j < T) ov[j] = *reinterpret_cast<const int2*>(my + 2 * j);
         auto load_step = [&](int t, float4& r0, float4& r1, float4& r2, float4& r3) {
-            const int2 o = *reinterpret_cast<const int2*>(my + 2 * t);
+            const int2 o = ov[t];  // t is a compile-time index (the step loop is unrolled)
             r0 = *reinterpret_cast<const float4*>(simg + o.x + clo);
             r1 = *reinterpret_cast<const float4*>(simg + o.x + chi);
             r2 = *reinterpret_cast<const float4*>(simg + o.y + clo);
@@ -1114,21 +1142,33 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
             acc[0] *= r2.x; acc[1] *= r2.y; acc[2] *= r2.z; acc[3] *= r2.w;
             acc[4] *= r3.x; acc[5] *= r3.y; acc[6] *= r3.z; acc[7] *= r3.w;
         };
-        float4 a0, a1, a2, a3, b0, b1, b2, b3;
-        load_step(0, a0, a1, a2, a3);
+        // ring of kPD steps: the reads of steps t+1 .. t+kPD-1 are in flight
+        // while step t is multiplied
+        constexpr int kPD = MODE == kModeFused ? 3 : 2;  // (multi-round modes also hold the next round's evidence)
+        float4 rb[kPD][4];
+        load_step(0, rb[0][0], rb[0][1], rb[0][2], rb[0][3]);
+        if (T > 1) load_step(1, rb[1][0], rb[1][1], rb[1][2], rb[1][3]);
         CBN_STAMP(4);
-        int t = 0;
-        for (; t + 2 <= T; t += 2) {
-            load_step(t + 1, b0, b1, b2, b3);
-            mul_step(a0, a1, a2, a3);
-            if (t + 2 < T) load_step(t + 2, a0, a1, a2, a3);
-            mul_step(b0, b1, b2, b3);
+#ifdef CBN_ABL_NOPROD
+        if (T > 0) mul_step(rb[0][0], rb[0][1], rb[0][2], rb[0][3]);
+#else
+#pragma unroll
+        for (int t = 0; t < 17; ++t) {
+            if (t < T) {  // wave-uniform
+                if (t + kPD - 1 < T && t + kPD - 1 < 17) {
+                    float4* n = rb[(t + kPD - 1) % kPD];
+                    load_step(t + kPD - 1 < 17 ? t + kPD - 1 : 16, n[0], n[1], n[2], n[3]);
+                }
+                const float4* c = rb[t % kPD];
+                mul_step(c[0], c[1], c[2], c[3]);
+            }
         }
-        if (t < T) mul_step(a0, a1, a2, a3);
+#endif
         CBN_STAMP(5);
         if (q < q1) {
             if (MODE == kModeFused) fq = q;
             if (MODE == kModeWrite || MODE == kModeRaw) {
+                // plain stores: the raw rows are re-read by the scale pass (L2 hits)
                 const float dv = MODE == kModeWrite ? maxv : 1.f;
                 float* o = out + q * N;
                 *reinterpret_cast<float4*>(o + clo) = MODE == kModeWrite
@@ -1166,7 +1206,11 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         __syncthreads();
         CBN_STAMP(7);
         if (wid == 0) {
+#ifdef CBN_ABL_NOBAR
+            const unsigned gm = __float_as_uint(wave_max(lane < kQueryThreads / kWave ? wmax[lane] : 0.f));
+#else
             const unsigned gm = slot_barrier_max(sync, epoch, wave_max(lane < kQueryThreads / kWave ? wmax[lane] : 0.f));
+#endif
             if (lane == 0) {
                 wmax[0] = __uint_as_float(gm);
                 if (blockIdx.x == 0 && max_out) *max_out = gm;
@@ -1177,9 +1221,9 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         CBN_STAMP(9);
         maxv = wmax[0];
         if (fq >= 0) {
-            float* o = out + fq * N;
-            *reinterpret_cast<float4*>(o + clo) = make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv);
-            *reinterpret_cast<float4*>(o + chi) = make_float4(acc[4] / maxv, acc[5] / maxv, acc[6] / maxv, acc[7] / maxv);
+            const int ob = (int)(fq - q0) * (N * 4);
+            store_wt(orsrc, ob + clo * 4, make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv));
+            store_wt(orsrc, ob + chi * 4, make_float4(acc[4] / maxv, acc[5] / maxv, acc[6] / maxv, acc[7] / maxv));
         }
         CBN_STAMP(10);
     }

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 out=continuousbayesiannetwork_amd/libcbn_amd_$name.so
 tmp=$(mktemp -d)
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -Wno-unused-result -I include"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -mllvm -amdgpu-kernarg-preload-count=16 -Wno-unused-result -I include"
 /opt/rocm/bin/hipcc $F "$@" -c -o $tmp/a.o continuousbayesiannetwork_amd/csrc/cbn_infer.hip &
 /opt/rocm/bin/hipcc $F "$@" -c -o $tmp/b.o continuousbayesiannetwork_amd/csrc/cbn_param.hip &
 wait %1 && wait %2
