@@ -49,6 +49,7 @@ from continuousbayesiannetwork_amd.distributed import ShardedStepper  # noqa: E4
 from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_PEAK_GBS = 7 * 153.0  # 7 xGMI links x ~153 GB/s per GPU (incoming), the reassembly's bound at N > 1
 
 
 def pmc_traffic(kernel: str):
@@ -88,6 +89,9 @@ def parse():
                     help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
     ap.add_argument("--exchange-every", type=int, default=8,
                     help="N>1: steps per all-reduce + scale group (1..8)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: keep each rank's rows (no all-gather reassembly of the [Q, N] marginal tensor); by "
+                         "default the step includes the reassembly and the rank-local step is reported beside it")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
@@ -148,8 +152,9 @@ def main():
     # of the block max words + the in-place scale run on a comm stream, once per
     # --exchange-every steps (8) for all of them, so the exchange overlaps the next steps' launches
     # (distributed.ShardedStepper)
+    gather = sharded and not a.no_gather
     stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                             force_exchange=sharded)
+                             force_exchange=sharded, gather=gather)
 
     def step():
         ev = batches[it[0] % len(batches)]
@@ -160,6 +165,23 @@ def main():
                 stepper.wait()
             return rows
         return bn.infer(target, ev, N_max=d)
+
+    def timed_steps(K):
+        """K steps between barriers + device syncs; max over ranks of the wall time."""
+        if sharded:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step()
+        stepper.wait()
+        torch.cuda.synchronize()
+        if sharded:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item())
 
     random.seed(0)
     for _ in range(a.warmup):
@@ -203,13 +225,18 @@ def main():
         tmax, twrite = tmax_ms * 1e-3, twrite_ms * 1e-3
         n_cols = len(names)  # evidence columns read per query
         bytes_q = Q * (4 * n_cols + 4 * d)  # evidence floats in + pdf row out
-        vpl = int(os.environ.get("CBN_FAST_VPL", "2"))
+        from continuousbayesiannetwork_amd import _native
+
+        plan = next(iter(bn.engine._plans.values()))
+        pflags = _native.load().cbn_plan_flags(plan.handle)
+        vpl = 2 if pflags & _native.CBN_PLAN_VPL2 else 1
         nptr = 128 if 4 * n <= 128 else 416  # kernel-argument pointer table sized to the plan (n factors)
         # the dominant kernel: fused single launch; beyond its capacity the raw
         # compute pass (then an HBM-bound scale); --two-pass: the write pass
         mode, what, t_dom = ((2, "single launch: both passes", twrite) if fused else
                              (1, "write pass", twrite) if a.two_pass else (3, "raw compute pass", tmax))
-        kname = f"k_query_fast<{vpl}, true, {mode}, {nptr}>"  # <VPL, LDS, MODE, NP>
+        kname = (f"k_query_staged<{mode}>" if pflags & _native.CBN_PLAN_STAGED
+                 else f"k_query_fast<{vpl}, true, {mode}, {nptr}>")  # <MODE> / <VPL, LDS, MODE, NP>
         achieved = bytes_q / t_dom / 1e9
         traffic, tsrc = pmc_traffic(kname)
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
@@ -221,6 +248,19 @@ def main():
                               else "HIP events around the launches of every 8th step (library-side)")
         if not fused:
             roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
+    elif sharded and gather and world > 1:
+        # with the reassembly, each rank receives the other ranks' rows every
+        # step over xGMI: (world - 1) x Q x 4N bytes -- the dominant transfer
+        t_step = ev0.elapsed_time(ev1) / K * 1e-3
+        bytes_in = (world - 1) * Q * 4 * d
+        achieved = bytes_in / t_step / 1e9
+        roofline = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / XGMI_PEAK_GBS, 4), traffic=None,
+                        kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of the "
+                               "[Q, N] rows (per step)",
+                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_in, timed_steps=K,
+                        timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
+                               "rows received from the other ranks per step")
     elif sharded:
         # sharded step (raw launch + all-reduce(max) of the block words + in-place
         # scale, overlapped across steps): per-GPU algorithmic bytes of one step =
@@ -232,9 +272,20 @@ def main():
         achieved = bytes_step / t_step / 1e9
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                        kernel="sharded step: k_query_fast raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
+                        kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
                         avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_step, timed_steps=K,
                         timing="HIP events on rank 0's launch stream around the timed region / K steps")
+
+    local = None
+    if sharded and gather:
+        # the same step without the reassembly (each rank keeps its rows), for reference
+        stepper.close()
+        stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
+                                 force_exchange=True, gather=False)
+        for _ in range(a.warmup):
+            step()
+        stepper.wait()
+        local = Q * world * K / timed_steps(K)
 
     cold = None
     if not sharded and not a.rebuild_tables:
@@ -264,7 +315,8 @@ def main():
                                    f"{n - 1} nodes, N_max={d}", "queries_per_gpu": Q, "global_batch": Q * world,
                        "parallelism": f"query-shard x{world}" + (
                            " + RCCL all-reduce(max) of the block max words" + (
-                               ", serial" if a.serial_exchange else ", overlapped with the next step's launch")
+                               ", serial" if a.serial_exchange else ", overlapped with the next step's launch") + (
+                               " + RCCL all-gather of the [Q, N] marginal tensor on every rank" if gather else "")
                            if sharded else "")},
             "roofline": roofline, "cpu_baseline": cpu,
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
@@ -272,6 +324,8 @@ def main():
         }
         if cold is not None:
             line["value_rebuild_tables"] = round(cold, 1)
+        if local is not None:
+            line["value_rank_local"] = round(local, 1)  # same step, each rank keeps its own rows (no all-gather)
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)

@@ -103,6 +103,8 @@ _SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "cbn_plan_fused_capacity": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "cbn_debug_flag_timeout": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbn_plan_flags": (ctypes.c_int32, [ctypes.c_void_p]),
     "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "cbn_scale_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_int32, ctypes.c_void_p]),
@@ -117,6 +119,9 @@ CBN_RUN_TIMED = 2
 CBN_RUN_TWO_PASS = 4
 CBN_RUN_RAW = 8
 CBN_E_UNSUPPORTED = -4
+CBN_E_TIMEOUT = -5
+CBN_PLAN_FAST, CBN_PLAN_LDS, CBN_PLAN_PAIRED, CBN_PLAN_STAGED = 1, 2, 4, 8
+CBN_PLAN_FUSED, CBN_PLAN_PARAMETRIC, CBN_PLAN_VPL2 = 16, 32, 64
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
@@ -175,11 +180,15 @@ def check(rc: int, what: str):
 
 
 def require_gpu(device) -> torch.device:
+    """The HIP device of ``device`` with an explicit index ("cuda" -> the
+    current device): the native entry points take the index as an int."""
     device = torch.device(device)
     if device.type != "cuda" or not torch.cuda.is_available():
         raise NativeError(
             f"the MI355X inference path needs a HIP device, got device={device!s} "
             f"(torch.cuda.is_available()={torch.cuda.is_available()})")
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     load()
     return device
 

@@ -5,6 +5,17 @@ from typing import Dict
 import torch
 
 
+# Bumped whenever any estimator's fitted state changes (fit, load_model, a
+# parameter edit followed by _invalidate): inference plans capture raw device
+# pointers to CPDs / packed weights, so the engine drops every cached plan when
+# the generation it was built under is stale (one integer compare per call).
+GENERATION = [0]
+
+
+def bump_generation():
+    GENERATION[0] += 1
+
+
 class BaseParameterLearningEstimator(ABC):
     def __init__(self, config: Dict, **kwargs):
         self.estimator_name = config.get("estimator_name")
@@ -18,6 +29,7 @@ class BaseParameterLearningEstimator(ABC):
     def fit(self, node_data: torch.Tensor, parents_data: torch.Tensor = None):
         """node_data [n_samples]; parents_data [n_parents_features, n_samples]."""
         self._fit(node_data, parents_data)
+        bump_generation()
 
     @abstractmethod
     def _fit(self, node_data: torch.Tensor, parents_data: torch.Tensor = None):

@@ -597,8 +597,15 @@ __device__ __forceinline__ unsigned slot_barrier_max(unsigned* __restrict__ sync
         if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kSpinLimit) {
-            if (lane == 0) atomicOr(&sync[2], 1u);
-            break;
+            // timed out: flag it on the device (cbn_plan_status) and in the plan's
+            // host-mapped status word (the next cbn_plan_run reports it), and make
+            // this block's rows NaN instead of dividing by a partial max
+            if (lane == 0) {
+                atomicOr(&sync[2], 1u);
+                unsigned* hs = *reinterpret_cast<unsigned* const*>(sync + kHostStatusWordOff);
+                if (hs) __hip_atomic_store(hs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return 0x7fc00000u;  // NaN
         }
     }
     return wave_max_u(gm);  // non-negative floats: unsigned order == float order
@@ -1506,7 +1513,16 @@ int cbn_debug_set_check_buffer(void* dev_ptr) {
 }
 #endif
 
+// Test hook: mark the plan's host-mapped status as if a fused launch had timed
+// out (the reporting path of CBN_E_TIMEOUT without starving the GPU).
+int cbn_debug_flag_timeout(cbn_plan* plan) {
+    if (!plan || !plan->h_status) return set_err(CBN_E_ARG, "cbn_debug_flag_timeout: plan has no status word");
+    __atomic_store_n(plan->h_status, 1u, __ATOMIC_RELEASE);
+    return CBN_OK;
+}
+
 #ifdef CBN_STAMPS
+
 int cbn_debug_set_stamp_buffer(void* dev_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)));
     return CBN_OK;
@@ -1752,6 +1768,16 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         ok = hipMemcpy(P->d_image + zero_off + 64, ones.data(), sizeof(float) * 64, hipMemcpyHostToDevice) == hipSuccess;
     }
     ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    // host-mapped status word of the fused launches' timeout (polled for free by cbn_plan_run);
+    // its device address lives in the sync buffer for the (rare) timeout path
+    ok = ok && hipHostMalloc(reinterpret_cast<void**>(&P->h_status), sizeof(unsigned),
+                             hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+    if (ok) {
+        *P->h_status = 0;
+        unsigned* dh = nullptr;
+        ok = hipHostGetDevicePointer(reinterpret_cast<void**>(&dh), P->h_status, 0) == hipSuccess &&
+             hipMemcpy(P->d_sync + kHostStatusWordOff, &dh, sizeof(dh), hipMemcpyHostToDevice) == hipSuccess;
+    }
     for (int sl = 0; ok && sl < ns; ++sl)
         ok = hipMemcpy(P->d_image + qs[sl].dom_off, slot_dom[sl], sizeof(float) * slot_card[sl],
                        hipMemcpyDeviceToDevice) == hipSuccess;
@@ -1865,6 +1891,7 @@ int cbn_plan_destroy(cbn_plan* plan) {
     if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);
     if (plan->d_sync) (void)hipFree(plan->d_sync);
+    if (plan->h_status) (void)hipHostFree(plan->h_status);
     if (plan->param) param_destroy(plan->param);
     delete plan;
     return CBN_OK;
@@ -1912,6 +1939,11 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
 int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
                  uint32_t* max_bits, float* out, int32_t flags, void* stream) {
     if (!plan) return set_err(CBN_E_ARG, "null plan");
+    if (plan->h_status && __atomic_load_n(plan->h_status, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(plan->h_status, 0u, __ATOMIC_RELEASE);
+        return set_err(CBN_E_TIMEOUT, "an earlier single-launch call of this plan timed out in its grid barrier "
+                                      "(not every block was resident); its rows are NaN");
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if (plan->param) {
@@ -2054,10 +2086,19 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
     unsigned v = 0;
     HIP_TRY(hipMemcpy(&v, plan->d_sync + 2, sizeof(unsigned), hipMemcpyDeviceToHost));
     *status = (int32_t)v;
+    if (plan->h_status) __atomic_store_n(plan->h_status, 0u, __ATOMIC_RELEASE);  // reported here
     return CBN_OK;
 }
 
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
+
+int32_t cbn_plan_flags(const cbn_plan* plan) {
+    if (!plan) return 0;
+    return (plan->fast ? CBN_PLAN_FAST : 0) | (plan->use_lds ? CBN_PLAN_LDS : 0) |
+           (plan->paired ? CBN_PLAN_PAIRED : 0) | (plan->staged ? CBN_PLAN_STAGED : 0) |
+           (plan->fused_ok ? CBN_PLAN_FUSED : 0) | (plan->param ? CBN_PLAN_PARAMETRIC : 0) |
+           (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0);
+}
 
 int32_t cbn_plan_max_words(const cbn_plan* plan) {
     if (plan && plan->param) return param_max_words(plan->param);

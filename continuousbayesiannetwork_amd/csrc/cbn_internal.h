@@ -22,6 +22,7 @@ constexpr int kFastPtrs = 416;  // fast table path: 104 factors x 4 observed par
 // kSlotWordOff, the fused barrier's slots: block b publishes {epoch, max} in
 // its own 8-byte slot and every block polls all of them.
 constexpr int kSyncLine = 32;
+constexpr int kHostStatusWordOff = 8;  // words 8-9 of line 0: device address of the plan's host-mapped status
 constexpr int kMaxSlots = 1024;
 constexpr int kSlotWordOff = kSyncLine;
 // then the max/raw passes' per-block maxima (one word per block; the
@@ -75,7 +76,8 @@ struct cbn_plan {
     bool paired = false;         // N = 32 bank-half layout (RS = 64, factor f in half f & 1), VPL 2 in LDS
     bool staged = false;         // paired plans of <= 32 factors: k_query_staged (evidence staged by factor)
     size_t staged_lds_bytes = 0;
-    int zero_off = -1;           // paired layout: float offset of the zero super-row (ones super-row at +64)
+    int zero_off = -1;
+    unsigned* h_status = nullptr;  // host-mapped: 1 after a fused launch timed out (reported by the next run)           // paired layout: float offset of the zero super-row (ones super-row at +64)
     unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;

@@ -77,14 +77,14 @@ bool gather(py::dict& evidence, py::tuple& slots, py::object& first, int64_t dev
     return true;
 }
 
+at::Tensor check_out(py::object& out_obj, int64_t n, int64_t n_samples, int64_t dev);
+
 py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots, py::object first,
                int64_t device_index, int64_t n_samples, bool target_observed, uintptr_t max_ptr, int32_t flags,
                py::object out_obj) {
     Cols c;
     if (!gather(evidence, slots, first, device_index, target_observed, c)) return py::none();
-    at::Tensor out = out_obj.is_none() ? at::empty({c.n, n_samples},
-                                                   at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_index))
-                                       : THPVariable_Unpack(out_obj.ptr());
+    at::Tensor out = check_out(out_obj, c.n, n_samples, device_index);
     const hipStream_t s = c10::hip::getCurrentHIPStream(device_index).stream();
     const int rc = reinterpret_cast<run_fn>(fn)(reinterpret_cast<void*>(plan), c.n, c.p,
                                                 (int32_t)PyTuple_GET_SIZE(slots.ptr()),
@@ -114,6 +114,10 @@ struct Rccl {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
 } g_rccl;
 
@@ -132,6 +136,10 @@ void rccl_load(const std::string& path) {
     g_rccl.comm_destroy = reinterpret_cast<decltype(g_rccl.comm_destroy)>(sym("ncclCommDestroy"));
     g_rccl.error_string = reinterpret_cast<decltype(g_rccl.error_string)>(sym("ncclGetErrorString"));
     g_rccl.all_reduce = reinterpret_cast<decltype(g_rccl.all_reduce)>(sym("ncclAllReduce"));
+    g_rccl.all_gather = reinterpret_cast<decltype(g_rccl.all_gather)>(sym("ncclAllGather"));
+    g_rccl.broadcast = reinterpret_cast<decltype(g_rccl.broadcast)>(sym("ncclBroadcast"));
+    g_rccl.group_start = reinterpret_cast<decltype(g_rccl.group_start)>(sym("ncclGroupStart"));
+    g_rccl.group_end = reinterpret_cast<decltype(g_rccl.group_end)>(sym("ncclGroupEnd"));
 }
 
 #define CBN_NCCL_OK(x)                                                                                   \
@@ -172,146 +180,353 @@ void nccl_comm_destroy(uintptr_t comm) {
 // ~50 us of host time per step, 4x the GPU time of a 65k-query raw launch).
 // Steps are exchanged in groups of G:
 //   compute stream A: raw launch of each step -> its words slot
-//   comm stream C:    after the group's G-th raw launch (ready event), ONE
-//                     ncclAllReduce(MAX) over the group's G x W words and ONE
-//                     cbn_scale_batch launch dividing each step's rows by its max
-// so the per-exchange host costs (event record + cross-stream wait ~5.5 us,
-// scale launch ~4.3 us, measured on MI355X by host_timing()) are paid once
-// per G steps.  Word slots form a ring of two groups; A waits for C only when
-// it starts a group whose slots the exchange two groups back still reads.
-// Rows are recorded on C for the caching allocator.  flush() (wait(),
+//   comm stream C:    after the group's last raw launch (hand-off), ONE
+//                     all-reduce(MAX) over the group's G x W words, ONE scale
+//                     launch dividing each step's rows by its own max, and --
+//                     with gather -- every step's all-gather of the rank shards
+//                     into the full [Q, N] marginal tensor
+// so the per-exchange host costs are paid once per G steps.  Word slots form a
+// ring of two groups (halves); A waits for C only when it starts a group in a
+// half whose previous exchange may still be reading it.  flush() (wait(),
 // synchronize()) exchanges a partial group.
+//
+// StepRing holds exactly that bookkeeping and nothing device-specific: the
+// device actions are an Ops object -- HipOps (HIP streams/events, RCCL,
+// cbn_scale_batch) for the GPU, PyOps (Python callbacks, CPU tensors) for the
+// world-size-2 gloo test that drives the same ring with partial groups,
+// wait() mid-group, empty and uneven shards.
+struct Slot {
+    int half;   // ring half of the group
+    int index;  // position in the group
+};
+
+template <class Ops>
+class StepRing {
+  public:
+    StepRing(Ops ops, int group) : ops_(std::move(ops)), G_(group < 1 ? 1 : (group > 8 ? 8 : group)) {}
+
+    // enqueue one step: `launch(slot)` writes the step's rows and its words slot
+    // (an empty shard zeroes the slot); `item` is what the exchange scales (and
+    // gathers) for it.  Returns 0 or a C ABI error code.
+    template <class Launch>
+    int step(Launch&& launch, typename Ops::Item item) {
+        const int half = (int)(g_ & 1);
+        if (pend_.empty() && used_[half]) ops_.wait_done(half);  // the exchange two groups back read this half
+        const Slot slot{half, (int)pend_.size()};
+        int rc = launch(slot);
+        if (rc) return rc;
+        pend_.push_back(std::move(item));
+        ++k_;
+        if ((int)pend_.size() == G_) return flush();
+        return 0;
+    }
+    int flush() {
+        if (pend_.empty()) return 0;
+        const int half = (int)(g_ & 1);
+        ops_.handoff();  // C waits for every raw launch of the group (enqueued on A)
+        int rc = ops_.exchange(half, (int)pend_.size());  // all-reduce(MAX) of the group's words
+        if (!rc) rc = ops_.scale(half, pend_);            // each step / its own global max
+        if (!rc) rc = ops_.gather(pend_);                 // optional: reassemble the full tensors
+        if (rc) return rc;
+        ops_.done(half, pend_);
+        used_[half] = true;
+        pend_.clear();
+        ++g_;
+        return 0;
+    }
+    // every enqueued exchange is ordered before the caller's later work
+    int wait() {
+        const int rc = flush();
+        if (!rc && k_) ops_.join();
+        return rc;
+    }
+    Ops& ops() { return ops_; }
+    int64_t steps() const { return k_; }
+    int group() const { return G_; }
+    int pending() const { return (int)pend_.size(); }
+
+  private:
+    Ops ops_;
+    int G_;
+    std::vector<typename Ops::Item> pend_;
+    bool used_[2] = {false, false};
+    int64_t k_ = 0, g_ = 0;
+};
+
+// What one step contributes to its group's exchange.
+struct StepItem {
+    at::Tensor rows;  // this rank's [q_r, N] rows (a view into `full` when gathering)
+    at::Tensor full;  // gather: the [Q, N] marginal tensor (undefined otherwise)
+    std::vector<int64_t> counts;  // gather: rows of every rank, rank order
+};
+
+// ---- GPU: HIP streams / events, RCCL, cbn_scale_batch
+struct HipOps {
+    using Item = StepItem;
+    scale_batch_fn scale_batch = nullptr;
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0;
+    int64_t dev = 0, W = 0;
+    int G = 1;
+    c10::hip::HIPStream cs;
+    at::Tensor words;  // [2G, W] int32 on the device
+    hipEvent_t ready = nullptr, tail = nullptr;
+    hipEvent_t done_ev[2] = {nullptr, nullptr};
+
+    HipOps(scale_batch_fn sb, ncclComm_t c, int world_, int rank_, int64_t dev_, int64_t W_, int G_)
+        : scale_batch(sb), comm(c), world(world_), rank(rank_), dev(dev_), W(W_), G(G_),
+          cs(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)dev_)) {
+        words = at::zeros({2 * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
+        CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));
+        for (auto& e : done_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HipOps(HipOps&& o) noexcept
+        : scale_batch(o.scale_batch), comm(o.comm), world(o.world), rank(o.rank), dev(o.dev), W(o.W), G(o.G),
+          cs(o.cs), words(std::move(o.words)), ready(o.ready), tail(o.tail) {
+        done_ev[0] = o.done_ev[0];
+        done_ev[1] = o.done_ev[1];
+        o.ready = o.tail = o.done_ev[0] = o.done_ev[1] = nullptr;
+    }
+    ~HipOps() {
+        if (ready) (void)hipEventDestroy(ready);
+        if (tail) (void)hipEventDestroy(tail);
+        for (auto e : done_ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    hipStream_t A() const { return c10::hip::getCurrentHIPStream(dev).stream(); }
+    int* slot_words(Slot s) { return words.data_ptr<int>() + ((int64_t)s.half * G + s.index) * W; }
+
+    void wait_done(int half) { CBN_HIP_OK(hipStreamWaitEvent(A(), done_ev[half], 0)); }
+    void handoff() {
+        CBN_HIP_OK(hipEventRecord(ready, A()));
+        CBN_HIP_OK(hipStreamWaitEvent(cs.stream(), ready, 0));
+    }
+    int exchange(int half, int nb) {
+        if (comm) {
+            int* w = words.data_ptr<int>() + (int64_t)half * G * W;
+            CBN_NCCL_OK(g_rccl.all_reduce(w, w, (size_t)nb * W, ncclInt32, ncclMax, comm, cs.stream()));
+        }
+        return 0;
+    }
+    int scale(int half, const std::vector<Item>& items) {
+        float* outs[8];
+        int64_t ns[8];
+        const int nb = (int)items.size();
+        for (int b = 0; b < nb; ++b) {
+            outs[b] = static_cast<float*>(items[b].rows.data_ptr());
+            ns[b] = items[b].rows.numel();
+        }
+        return scale_batch(outs, ns, nb, reinterpret_cast<const unsigned*>(words.data_ptr<int>() + (int64_t)half * G * W),
+                           (int32_t)W, cs.stream());
+    }
+    // all-gather of every step's shards into its full tensor: equal shards ->
+    // ncclAllGather in place; uneven -> one ncclBroadcast per rank (root r sends
+    // its rows to their offset in every rank's full tensor), all in one group
+    int gather(const std::vector<Item>& items) {
+        bool any = false;
+        for (const auto& it : items) any |= it.full.defined();
+        if (!any) return 0;
+        if (!comm || world == 1) return 0;  // one rank: rows already in place
+        CBN_NCCL_OK(g_rccl.group_start());
+        for (const auto& it : items) {
+            if (!it.full.defined()) continue;
+            float* full = static_cast<float*>(it.full.data_ptr());
+            const int64_t N = it.full.size(1);
+            bool equal = true;
+            for (int r = 1; r < world; ++r) equal &= it.counts[r] == it.counts[0];
+            if (equal) {
+                const size_t cnt = (size_t)(it.counts[0] * N);
+                CBN_NCCL_OK(g_rccl.all_gather(full + (int64_t)rank * cnt, full, cnt, ncclFloat32, comm, cs.stream()));
+            } else {
+                int64_t off = 0;
+                for (int r = 0; r < world; ++r) {
+                    const size_t cnt = (size_t)(it.counts[r] * N);
+                    CBN_NCCL_OK(g_rccl.broadcast(full + off * N, full + off * N, cnt, ncclFloat32, r, comm,
+                                                 cs.stream()));
+                    off += it.counts[r];
+                }
+            }
+        }
+        CBN_NCCL_OK(g_rccl.group_end());
+        return 0;
+    }
+    void done(int half, const std::vector<Item>& items) {
+        CBN_HIP_OK(hipEventRecord(done_ev[half], cs.stream()));
+        // rows / full tensors are used on C: the caching allocator must not recycle them early
+        for (const auto& it : items) {
+            c10::hip::HIPCachingAllocator::recordStream(it.rows.storage().data_ptr(), cs);
+            if (it.full.defined()) c10::hip::HIPCachingAllocator::recordStream(it.full.storage().data_ptr(), cs);
+        }
+    }
+    void join() {
+        CBN_HIP_OK(hipEventRecord(tail, cs.stream()));
+        CBN_HIP_OK(hipStreamWaitEvent(A(), tail, 0));
+    }
+};
+
+at::Tensor check_out(py::object& out_obj, int64_t n, int64_t n_samples, int64_t dev) {
+    if (out_obj.is_none())
+        return at::empty({n, n_samples}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+    if (!THPVariable_Check(out_obj.ptr())) throw std::invalid_argument("out must be a torch tensor");
+    at::Tensor out = THPVariable_Unpack(out_obj.ptr());
+    if (out.scalar_type() != at::kFloat || !out.is_cuda() || out.get_device() != dev || !out.is_contiguous() ||
+        out.dim() != 2 || out.size(0) != n || out.size(1) != n_samples ||
+        reinterpret_cast<uintptr_t>(out.data_ptr()) % 16)
+        throw std::invalid_argument("out must be a contiguous, 16-B aligned float32 [" + std::to_string(n) + ", " +
+                                    std::to_string(n_samples) + "] tensor on cuda:" + std::to_string(dev));
+    return out;
+}
+
 class Stepper {
   public:
     Stepper(uintptr_t run_addr, uintptr_t scale_batch_addr, uintptr_t plan, py::tuple slots, py::object first,
             int64_t device_index, int64_t n_samples, bool target_observed, int64_t n_words, int group,
-            uintptr_t comm)
-        : run_(reinterpret_cast<run_fn>(run_addr)), scale_batch_(reinterpret_cast<scale_batch_fn>(scale_batch_addr)),
-          plan_(reinterpret_cast<void*>(plan)), slots_(slots), first_(first), dev_(device_index),
-          n_samples_(n_samples), target_observed_(target_observed), W_(n_words),
-          G_(group < 1 ? 1 : (group > 8 ? 8 : group)), comm_(reinterpret_cast<ncclComm_t>(comm)),
-          cs_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_index)) {
-        words_ = at::zeros({2 * G_, W_}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev_));
-        CBN_HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-        for (auto& e : done_) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        CBN_HIP_OK(hipEventCreateWithFlags(&tail_, hipEventDisableTiming));
-    }
-    ~Stepper() {
-        (void)hipEventDestroy(ready_);
-        for (auto e : done_) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(tail_);
-    }
+            uintptr_t comm, int world, int rank)
+        : run_(reinterpret_cast<run_fn>(run_addr)), plan_(reinterpret_cast<void*>(plan)), slots_(slots),
+          first_(first), dev_(device_index), n_samples_(n_samples), target_observed_(target_observed),
+          ring_(HipOps(reinterpret_cast<scale_batch_fn>(scale_batch_addr), reinterpret_cast<ncclComm_t>(comm), world,
+                       rank, device_index, n_words, group < 1 ? 1 : (group > 8 ? 8 : group)),
+                group) {}
 
     // rows (final once this step's group has been exchanged and scaled on the
-    // comm stream -- after wait()), None when a fast check failed, or an int
-    // error code from the C ABI.
-    py::object step(py::dict evidence, py::object out_obj, int32_t flags) {
+    // comm stream -- after wait()); with counts (every rank's rows of this
+    // step, rank order): the full [sum(counts), N] tensor, this rank's rows
+    // written at its offset and the others' all-gathered into it.  None when a
+    // fast check failed (the caller converts the evidence and retries), or an
+    // int error code from the C ABI.
+    py::object step(py::dict evidence, py::object out_obj, int32_t flags, py::object counts_obj) {
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
         Cols c;
-        if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return py::none();
-        const hipStream_t A = c10::hip::getCurrentHIPStream(dev_).stream();
-        const int half = (int)(g_ & 1);
-        if (pend_.empty() && used_[half]) CBN_HIP_OK(hipStreamWaitEvent(A, done_[half], 0));
-        at::Tensor out = out_obj.is_none()
-                             ? at::empty({c.n, n_samples_}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev_))
-                             : THPVariable_Unpack(out_obj.ptr());
-        int* w = words_.data_ptr<int>() + ((int64_t)half * G_ + (int64_t)pend_.size()) * W_;
+        int64_t n = 0;
+        if (!gather_cols(evidence, c, n)) return py::none();
+        HipOps& ops = ring_.ops();
+        StepItem item;
+        if (!counts_obj.is_none()) {
+            item.counts = counts_obj.cast<std::vector<int64_t>>();
+            if ((int)item.counts.size() != ops.world || item.counts[ops.rank] != n)
+                throw std::invalid_argument("counts must hold every rank's rows of this step (this rank: " +
+                                            std::to_string(n) + ")");
+            int64_t total = 0, lo = 0;
+            for (int r = 0; r < ops.world; ++r) {
+                if (r == ops.rank) lo = total;
+                total += item.counts[r];
+            }
+            item.full = out_obj.is_none()
+                            ? at::empty({total, n_samples_}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev_))
+                            : check_out(out_obj, total, n_samples_, dev_);
+            item.rows = item.full.narrow(0, lo, n);
+        } else {
+            item.rows = check_out(out_obj, n, n_samples_, dev_);
+        }
         const auto t1 = clk::now();
-        int rc = run_(plan_, c.n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()), reinterpret_cast<unsigned*>(w),
-                      static_cast<float*>(out.data_ptr()), flags, A);
+        at::Tensor ret = item.full.defined() ? item.full : item.rows;
+        float* rows = static_cast<float*>(item.rows.data_ptr());
+        int rc = ring_.step(
+            [&](Slot s) -> int {
+                int* w = ops.slot_words(s);
+                if (n == 0) {  // empty shard: contributes zero words, still joins the group's collectives
+                    CBN_HIP_OK(hipMemsetAsync(w, 0, sizeof(int) * ops.W, ops.A()));
+                    return 0;
+                }
+                return run_(plan_, n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()), reinterpret_cast<unsigned*>(w),
+                            rows, flags, ops.A());
+            },
+            std::move(item));
         if (rc) return py::int_(rc);
         const auto t2 = clk::now();
-        pend_.push_back(out);
-        ++k_;
-        if ((int)pend_.size() == G_) {
-            rc = flush_();
-            if (rc) return py::int_(rc);
-        }
-        py::object r = py::cast(out);
-        const auto t3 = clk::now();
         tacc_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
         tacc_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
-        tacc_[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
         ++tn_;
-        return r;
+        return py::cast(ret);
     }
 
-    // exchange + scale the pending partial group, then the current stream
-    // waits for every enqueued exchange
-    void wait() {
-        check_(flush_());
-        if (!k_) return;
-        CBN_HIP_OK(hipEventRecord(tail_, cs_.stream()));
-        CBN_HIP_OK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(dev_).stream(), tail_, 0));
-    }
+    void wait() { check_(ring_.wait()); }
     void synchronize() {
-        check_(flush_());
-        CBN_HIP_OK(hipStreamSynchronize(cs_.stream()));
+        check_(ring_.flush());
+        CBN_HIP_OK(hipStreamSynchronize(ring_.ops().cs.stream()));
     }
-    uintptr_t comm_stream() const { return reinterpret_cast<uintptr_t>(cs_.stream()); }
-    int64_t steps() const { return k_; }
-    int group() const { return G_; }
+    uintptr_t comm_stream() { return reinterpret_cast<uintptr_t>(ring_.ops().cs.stream()); }
+    int64_t steps() const { return ring_.steps(); }
+    int group() const { return ring_.group(); }
 
-    // mean host microseconds per step: gather + alloc, raw launch, the
-    // step's share of the group exchange (event, ncclAllReduce, scale) + return
+    // mean host microseconds per step: gather + alloc, launch + the step's
+    // share of the group exchange (hand-off, all-reduce, scale, all-gathers)
     std::vector<double> host_timing() {
-        std::vector<double> r(3, 0.0);
-        for (int i = 0; i < 3; ++i) r[i] = tn_ ? tacc_[i] / tn_ : 0.0;
+        std::vector<double> r(2, 0.0);
+        for (int i = 0; i < 2; ++i) r[i] = tn_ ? tacc_[i] / tn_ : 0.0;
         tacc_.fill(0.0);
         tn_ = 0;
         return r;
     }
 
   private:
-    int flush_() {
-        if (pend_.empty()) return 0;
-        const hipStream_t A = c10::hip::getCurrentHIPStream(dev_).stream();
-        const hipStream_t C = cs_.stream();
-        const int half = (int)(g_ & 1);
-        const int nb = (int)pend_.size();
-        int* w = words_.data_ptr<int>() + (int64_t)half * G_ * W_;
-        CBN_HIP_OK(hipEventRecord(ready_, A));
-        CBN_HIP_OK(hipStreamWaitEvent(C, ready_, 0));
-        if (comm_) CBN_NCCL_OK(g_rccl.all_reduce(w, w, (size_t)nb * W_, ncclInt32, ncclMax, comm_, C));
-        float* outs[8];
-        int64_t ns[8];
-        for (int b = 0; b < nb; ++b) {
-            outs[b] = static_cast<float*>(pend_[b].data_ptr());
-            ns[b] = pend_[b].numel();
+    // like gather(), but an empty shard is a valid step (n = 0)
+    bool gather_cols(py::dict& evidence, Cols& c, int64_t& n) {
+        if (!first_.is_none()) {
+            PyObject* f = PyDict_GetItem(evidence.ptr(), first_.ptr());
+            if (f && THPVariable_Check(f)) {
+                const at::Tensor& t = THPVariable_Unpack(f);
+                if (t.dim() >= 1 && t.size(0) == 0) {
+                    n = 0;
+                    return true;
+                }
+            }
         }
-        const int rc = scale_batch_(outs, ns, nb, reinterpret_cast<const unsigned*>(w), (int32_t)W_, C);
-        if (rc) return rc;
-        CBN_HIP_OK(hipEventRecord(done_[half], C));
-        used_[half] = true;
-        for (auto& t : pend_) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), cs_);
-        pend_.clear();
-        ++g_;
-        return 0;
+        if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return false;
+        n = c.n;
+        return true;
     }
     static void check_(int rc) {
         if (rc) throw std::runtime_error("cbn_scale_batch failed (rc=" + std::to_string(rc) + ")");
     }
 
     run_fn run_;
-    scale_batch_fn scale_batch_;
     void* plan_;
     py::tuple slots_;
     py::object first_;
     int64_t dev_, n_samples_;
     bool target_observed_;
-    int64_t W_;
-    int G_;
-    ncclComm_t comm_;
-    c10::hip::HIPStream cs_;
-    at::Tensor words_;
-    std::vector<at::Tensor> pend_;
-    hipEvent_t ready_ = nullptr, tail_ = nullptr;
-    hipEvent_t done_[2] = {nullptr, nullptr};
-    bool used_[2] = {false, false};
-    int64_t k_ = 0, g_ = 0;
-    std::array<double, 3> tacc_{};
+    StepRing<HipOps> ring_;
+    std::array<double, 2> tacc_{};
     int64_t tn_ = 0;
+};
+
+// ---- CPU test double: the same ring driven by Python callbacks
+//   launch(slot_half, slot_index, payload) -> None   (rows + words of the step)
+//   exchange(half, n_steps)                          (all-reduce of the group's words)
+//   scale(half, [payload, ...])                      (divide each step's rows)
+//   gather([payload, ...])                           (reassemble full tensors)
+//   and the ordering hooks wait_done(half), handoff(), done(half), join() --
+// the test logs every call and checks the ring's protocol from the log.
+struct PyOps {
+    using Item = py::object;
+    py::object cb;  // an object with the methods above
+    void wait_done(int half) { cb.attr("wait_done")(half); }
+    void handoff() { cb.attr("handoff")(); }
+    int exchange(int half, int nb) { return cb.attr("exchange")(half, nb).cast<int>(); }
+    int scale(int half, const std::vector<Item>& items) { return cb.attr("scale")(half, py::cast(items)).cast<int>(); }
+    int gather(const std::vector<Item>& items) { return cb.attr("gather")(py::cast(items)).cast<int>(); }
+    void done(int half, const std::vector<Item>&) { cb.attr("done")(half); }
+    void join() { cb.attr("join")(); }
+};
+
+class CpuStepRing {
+  public:
+    CpuStepRing(py::object cb, int group) : ring_(PyOps{cb}, group) {}
+    int step(py::object payload) {
+        py::object cb = ring_.ops().cb;
+        return ring_.step([&](Slot s) -> int { return cb.attr("launch")(s.half, s.index, payload).cast<int>(); },
+                          payload);
+    }
+    int wait() { return ring_.wait(); }
+    int flush() { return ring_.flush(); }
+    int pending() const { return ring_.pending(); }
+    int group() const { return ring_.group(); }
+
+  private:
+    StepRing<PyOps> ring_;
 };
 
 // cbn_scale on the current stream of out's device (sharded path, after the
@@ -333,7 +548,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("nccl_comm_destroy", &nccl_comm_destroy);
     py::class_<Stepper>(m, "Stepper")
         .def(py::init<uintptr_t, uintptr_t, uintptr_t, py::tuple, py::object, int64_t, int64_t, bool, int64_t, int,
-                      uintptr_t>())
+                      uintptr_t, int, int>())
         .def("step", &Stepper::step)
         .def("wait", &Stepper::wait)
         .def("synchronize", &Stepper::synchronize)
@@ -341,4 +556,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("steps", &Stepper::steps)
         .def("group", &Stepper::group)
         .def("host_timing", &Stepper::host_timing);
+    py::class_<CpuStepRing>(m, "CpuStepRing")
+        .def(py::init<py::object, int>())
+        .def("step", &CpuStepRing::step)
+        .def("wait", &CpuStepRing::wait)
+        .def("flush", &CpuStepRing::flush)
+        .def("pending", &CpuStepRing::pending)
+        .def("group", &CpuStepRing::group);
 }

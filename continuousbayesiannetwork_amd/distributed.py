@@ -79,16 +79,36 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
     write pass.
     """
     eng = bn.engine
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
     raw = eng.infer_raw(target_node, evidence_shard, N_max, out)
-    if raw is not None:
+    if raw is None and multi and eng.raw_fast_path(target_node, evidence_shard, N_max) is not None:
+        # an empty shard on a raw-capable plan: no rows, zero max words -- the
+        # same collectives as the other ranks
+        fp = eng.raw_fast_path(target_node, evidence_shard, N_max)
+        n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
+        if n == 0:
+            plan = fp.plan
+            rows = torch.empty((0, plan.n_samples), dtype=torch.float32, device=fp.device)
+            bits = torch.zeros_like(fp.words)
+            raw = (rows, plan.target_domain.unsqueeze(0).expand(0 if plan.target_observed else 1, -1), bits,
+                   lambda r, b: r)
+    # the path must be the same on every rank (different collectives would hang):
+    # take the raw path only where every rank can
+    ok = torch.tensor([1 if raw is not None else 0], dtype=torch.int32)
+    if multi:
+        if dist.get_backend(group) == "nccl":
+            ok = ok.to(torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()) == 1:
         rows, tdom, bits, scale = raw
-        multi = dist.is_initialized() and dist.get_world_size(group) > 1
         if multi:
             dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
         scale(rows, bits)
         if gather and multi:
             rows = gather_rows(rows, group)
         return rows, tdom
+    if raw is not None:  # this rank launched a raw pass another rank cannot take: redo it two-pass
+        torch.cuda.current_stream().synchronize()
     plan, cols, nq, tdom, device = eng.prepare(target_node, evidence_shard, N_max)
     if out is None:
         out = torch.empty((nq, plan.n_samples), dtype=torch.float32, device=device)
@@ -114,32 +134,43 @@ class ShardedStepper:
     stepper's comm stream: wait for the group's last launch, ONE
     ``ncclAllReduce(MAX)`` over the group's G x W words on our own RCCL
     communicator, ONE ``cbn_scale_batch`` launch dividing each step's rows by
-    its own global max.  The per-exchange host costs (event + cross-stream
-    wait, scale launch: ~10 us on MI355X) are paid once per G steps and the
-    RCCL latency hides behind the next group's launches.  (The same
-    choreography in Python -- events, stream switch, c10d all_reduce,
-    record_stream -- cost ~50 us of host time per step:
-    tools/shard_step_probe.py.)
+    its own global max, and -- ``gather=True``, the north star's reassembly --
+    each step's RCCL all-gather of the rank shards into the full [Q, N]
+    marginal tensor over xGMI (in place: a rank's raw launch writes its rows at
+    its offset of the full tensor; equal shards: ncclAllGather, uneven: one
+    ncclBroadcast per rank in one group).  The per-exchange host costs are
+    paid once per G steps and the RCCL latency hides behind the next group's
+    launches.  (The same choreography in Python -- events, stream switch, c10d
+    all_reduce, record_stream -- cost ~50 us of host time per step:
+    tools/shard_step_probe.py.)  The ring/group bookkeeping is
+    ``StepRing`` (csrc/host_fast.cpp), exercised on CPU by a world-size-2 gloo
+    test through the same class (``_cbn_host.CpuStepRing``).
 
     A step's rows are final once its group has been exchanged: call
     ``wait()`` (exchanges a partial group; the current stream then waits for
     the comm stream) before reading them.  Results equal ``sharded_infer`` (and
     the single-process ``infer`` on the concatenated batch) bit for bit.
     Every rank calls ``step`` and ``wait`` the same number of times, in the
-    same order (the exchanges are collectives).  Plans without a raw launch,
-    and evidence the native checks reject, fall back to the serial
-    ``sharded_infer`` (c10d collectives) after flushing the pending group.
+    same order (the exchanges are collectives); an empty shard is a valid step
+    (zero max words, no rows), and evidence the native checks reject is
+    converted and goes through the same ring, so no rank leaves the pipeline
+    on its own.  Plans without a raw launch use the serial ``sharded_infer``.
     """
 
     def __init__(self, bn, target_node: str, N_max: int = 16, group=None, exchange_every: int = 4,
-                 force_exchange: bool = False):
+                 force_exchange: bool = False, gather: bool = False):
         self.bn, self.target, self.N_max, self.group = bn, target_node, N_max, group
         self.G = max(1, min(8, exchange_every))
         # force_exchange: all-reduce even at world size 1 (exercises RCCL on one GPU)
-        self.exchange = force_exchange or (dist.is_initialized() and dist.get_world_size(group) > 1)
+        multi = dist.is_initialized() and dist.get_world_size(group) > 1
+        self.exchange = force_exchange or multi
+        self.world = dist.get_world_size(group) if multi else 1
+        self.rank = dist.get_rank(group) if multi else 0
+        self.gather = gather
         self._c = None
         self._fp = None
         self._comm = 0
+        self._serial = False
 
     def _setup(self, evidence_shard) -> bool:
         import ctypes
@@ -165,31 +196,56 @@ class ShardedStepper:
         plan = fp.plan
         scale_batch = ctypes.cast(_native.load().cbn_scale_batch, ctypes.c_void_p).value
         self._c = host.Stepper(fp.run_fn, scale_batch, plan.handle.value, fp.slot_keys, fp.first, fp.device.index,
-                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.G, self._comm)
+                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.G, self._comm,
+                               self.world, self.rank)
         self._fp = fp
         return True
 
-    def step(self, evidence_shard: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None):
-        if self._c is None and not self._setup(evidence_shard):
-            return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, out=out)
+    def _counts(self, n: int, total_rows: Optional[int]):
+        if not self.gather:
+            return None
+        if total_rows is None:  # equal shards
+            return [n] * self.world
+        return [shard_bounds(total_rows, self.world, r)[1] - shard_bounds(total_rows, self.world, r)[0]
+                for r in range(self.world)]
+
+    def step(self, evidence_shard: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None,
+             total_rows: Optional[int] = None):
+        """One step on this rank's shard.  ``gather=True``: returns the full
+        [Q, N] tensor (Q = ``total_rows``, the whole batch split by
+        ``shard_bounds``; None = equal shards), otherwise this rank's rows."""
+        if self._c is None and not self._serial and not self._setup(evidence_shard):
+            self._serial = True  # the plan has no raw launch: every rank decides alike (plan-level)
+        if self._serial:
+            return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, gather=self.gather,
+                                 out=out)
         fp = self._fp
-        res = self._c.step(evidence_shard, out, self.bn.engine.raw_flags(fp.plan))
-        if res is None:
-            self.wait()
-            return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, out=out)
+        n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
+        counts = self._counts(n, total_rows)
+        flags = self.bn.engine.raw_flags(fp.plan)
+        res = self._c.step(evidence_shard, out, flags, counts)
+        if res is None:  # dtype / device / layout the native checks reject: convert, same ring
+            cols = {k: evidence_shard[k] for k in fp.slot_keys}
+            conv = {k: v.to(device=fp.device, dtype=torch.float32).contiguous() for k, v in cols.items()}
+            for k, v in conv.items():
+                if v.dim() != 2:
+                    raise AssertionError("Each query tensor must be of dimension 2.")
+            res = self._c.step(conv, out, flags, counts)
+            if res is None:
+                raise ValueError("ShardedStepper.step: evidence batch rejected (shape / target-unobserved batch > 1)")
         if type(res) is int:
             from . import _native
 
             _native.check(res, "cbn_plan_run(raw)")
-        n = res.shape[0]
-        tdom = fp.tdom.get(n)
+        m = res.shape[0]
+        tdom = fp.tdom.get(m)
         if tdom is None:
             plan = fp.plan
-            tdom = fp.tdom[n] = plan.target_domain.unsqueeze(0).expand(n if plan.target_observed else 1, -1)
+            tdom = fp.tdom[m] = plan.target_domain.unsqueeze(0).expand(m if plan.target_observed else 1, -1)
         return res, tdom
 
     def wait(self):
-        """Make the current stream wait for every enqueued exchange + scale."""
+        """Make the current stream wait for every enqueued exchange + scale (+ gathers)."""
         if self._c is not None:
             self._c.wait()
 

@@ -29,6 +29,7 @@ import torch
 
 from .. import _native
 from .._native import CBN_FACTOR_QUERY, CBN_FACTOR_SCALAR, CBN_FACTOR_SHARED, CBN_MAX_EVIDENCE, CBN_MAX_PARENTS
+from ..base.parameter_learning import GENERATION
 
 
 def domain_index(values: torch.Tensor, domain: torch.Tensor) -> torch.Tensor:
@@ -154,6 +155,15 @@ class InferenceEngine:
         # batch fits one round of the resident grid; False forces two launches
         self.fused = True
         self._fast: Dict[tuple, "_FastPath"] = {}
+        self._gen = GENERATION[0]  # estimator generation the cached plans were built under
+
+    def _check_generation(self):
+        """Drop every cached plan when any estimator was refitted / reloaded /
+        edited since they were built (plans hold raw device pointers to the
+        CPDs and packed weights of that state)."""
+        if GENERATION[0] != self._gen:
+            self.invalidate()
+            self._gen = GENERATION[0]
 
     def invalidate(self):
         if self._plans:
@@ -190,6 +200,8 @@ class InferenceEngine:
                 est = self.bn.nodes_obj[spec.node].estimator
                 cpd = est.compiled()
                 doms = est.domains
+                # the plan's descriptors point into these: keep them alive with the plan
+                keep += [cpd, est.node_marginal, *doms]
                 d = descs[f]
                 d.kind = spec.kind
                 d.n_parents = len(spec.parents)
@@ -271,6 +283,7 @@ class InferenceEngine:
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
 
     def plan(self, target: str, observed: frozenset, N: int, device) -> Plan:
+        self._check_generation()
         key = (target, observed, int(N))
         p = self._plans.get(key)
         if p is not None:
@@ -324,6 +337,8 @@ class InferenceEngine:
               out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         # lean path: (target, evidence keys, N) -> cached deterministic plan
         key = (target, tuple(evidence.keys()), N_max)  # evidence=None raises AttributeError, as the reference
+        if GENERATION[0] != self._gen:
+            self._check_generation()
         fp = self._fast.get(key)
         if fp is not None:
             res = self._run_fast(fp, evidence, out)
@@ -410,6 +425,8 @@ class InferenceEngine:
         """The cached fast path of (target, evidence keys, N) when its plan takes
         raw launches (planned here if needed, nothing launched); else None."""
         key = (target, tuple(evidence.keys()), N_max)
+        if GENERATION[0] != self._gen:
+            self._check_generation()
         fp = self._fast.get(key)
         if fp is None:
             device = _native.require_gpu(self.bn.device)

@@ -30,7 +30,7 @@ from torch import nn
 from tqdm import tqdm
 
 from .. import _native
-from ..base.parameter_learning import BaseParameterLearningEstimator
+from ..base.parameter_learning import BaseParameterLearningEstimator, bump_generation
 
 
 def config_torch_optimizer(model, config: Dict = None):
@@ -77,6 +77,7 @@ class _Parametric(BaseParameterLearningEstimator):
     # ---- packing ----
     def _invalidate(self):
         self._packed = None
+        bump_generation()  # cached inference plans hold the old packed weights
 
     def _scale_norm(self) -> Tuple[float, float]:
         """sigma / s and the Gaussian normaliser as the reference computes them

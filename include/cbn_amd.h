@@ -29,6 +29,9 @@ extern "C" {
 #define CBN_E_HIP -2
 #define CBN_E_LIMIT -3
 #define CBN_E_UNSUPPORTED -4  /* the plan cannot take this launch mode (caller picks another) */
+#define CBN_E_TIMEOUT -5      /* an earlier single-launch call of this plan timed out in its grid barrier
+                                 (not every block was resident): that call's rows are NaN; reported (and
+                                 cleared) by the plan's next cbn_plan_run / cbn_plan_status */
 
 /* Factor kinds of bayesian_network.py:271-294 (the per-node `x` multiplied
  * into out_pdf):
@@ -153,6 +156,21 @@ int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, vo
 int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batches, const uint32_t* max_bits,
                     int32_t n_max, void* stream);
 int cbn_plan_status(cbn_plan* plan, int32_t* status);
+
+/* Which kernels serve the plan (bit set): diagnostics / bench labels. */
+#define CBN_PLAN_FAST 1        /* table fast path (k_query_fast / k_query_staged) */
+#define CBN_PLAN_LDS 2         /* the table image is staged in LDS (else read from L2 / HBM) */
+#define CBN_PLAN_PAIRED 4      /* N = 32 bank-half table layout */
+#define CBN_PLAN_STAGED 8      /* k_query_staged (evidence staged by factor) */
+#define CBN_PLAN_FUSED 16      /* single-launch (grid barrier) path available */
+#define CBN_PLAN_PARAMETRIC 32 /* parametric CPDs (cbn_param.hip) */
+#define CBN_PLAN_VPL2 64       /* 8 output columns per lane */
+int32_t cbn_plan_flags(const cbn_plan* plan);
+
+/* Test hook: mark the plan as if a single-launch call had timed out in its
+ * grid barrier, so the next cbn_plan_run returns CBN_E_TIMEOUT (exercises the
+ * reporting path without starving the GPU).  No reference counterpart. */
+int cbn_debug_flag_timeout(cbn_plan* plan);
 
 /* Average device time (ms) of the max and write passes over the timed calls
  * since the last read; waits for them; resets the ring. */

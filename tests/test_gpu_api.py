@@ -1,0 +1,127 @@
+"""API-level behaviour of the HIP engine that the parity tests do not reach:
+the default ``device="cuda"`` (no index), stale plans after a refit, the
+timeout reporting of the single-launch path, caller-supplied ``out``
+validation, and the pipelined sharded stepper with the all-gather reassembly
+(one rank over RCCL).  Tolerance where values are compared: rtol 1e-5, atol
+1e-7 (north star)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from continuousbayesiannetwork_amd import BayesianNetwork, _native
+from helpers import chain_data, make_bn, sample_evidence
+from oracle.ref_infer import OracleBN
+
+pytestmark = pytest.mark.gpu
+RTOL, ATOL = 1e-5, 1e-7
+
+
+def _t(ev, dev):
+    return {k: torch.tensor(v, device=dev) for k, v in ev.items()}
+
+
+def test_default_cuda_device_without_index(gpu):
+    """BayesianNetwork(device="cuda") (the reference's default form): infer
+    twice (the cached native fast path), infer_raw and the stepper all work."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper
+
+    data, cols, edges = chain_data(8, 8, 5000, 4, stay=0.7)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device="cuda")
+    names = [c for c in cols if c != "X7"]
+    ev = _t(sample_evidence(data, cols, names, 777, 2), "cuda")
+    a, _ = bn.infer("X7", ev, N_max=8)
+    b, _ = bn.infer("X7", ev, N_max=8)
+    ref, _ = OracleBN(edges, cols, data).infer("X7", {k: v.cpu().numpy() for k, v in ev.items()}, 8)
+    np.testing.assert_allclose(a.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    rows, _, words, scale = bn.engine.infer_raw("X7", ev, 8)
+    scale(rows, words)
+    np.testing.assert_array_equal(rows.cpu().numpy(), a.cpu().numpy())
+    st = ShardedStepper(bn, "X7", 8, exchange_every=2)
+    r, _ = st.step(ev)
+    st.wait()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r.cpu().numpy(), a.cpu().numpy())
+    st.close()
+
+
+def test_refit_drops_cached_plans(gpu):
+    """A node refitted on other data after a cached infer: the next infer
+    follows the new CPD (plans hold raw pointers into the old one)."""
+    from oracle.ref_infer import OracleNode
+
+    data, cols, edges = chain_data(6, 4, 4000, 5, stay=0.8)
+    data2, _, _ = chain_data(6, 4, 4000, 6, stay=0.3)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = sample_evidence(data, cols, ["X4", "X2"], 300, 3)
+    bn.infer("X5", _t(ev, gpu), N_max=4)
+    bn.infer("X5", _t(ev, gpu), N_max=4)
+    # refit X5 | X4 on the second data set through the Node API
+    y, x = data2[:, cols.index("X5")], data2[:, cols.index("X4")][None, :]
+    bn.nodes_obj["X5"].fit(torch.tensor(y, device=gpu), torch.tensor(x, device=gpu))
+    got, _ = bn.infer("X5", _t(ev, gpu), N_max=4)
+    ora = OracleBN(edges, cols, data)
+    node = OracleNode("X5", ["X4"])
+    node.fit(y, x)
+    ora.nodes["X5"] = node
+    ref, _ = ora.infer("X5", ev, 4)
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
+def test_timeout_is_reported_on_next_call(gpu):
+    """A fused launch that timed out in its grid barrier (simulated through the
+    test hook) is reported by the plan's next call as CBN_E_TIMEOUT (NativeError),
+    and cleared."""
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    ev = _t(sample_evidence(data, cols, names, 4096, 9), gpu)
+    a, _ = bn.infer("X19", ev, N_max=32)
+    plan = next(iter(bn.engine._plans.values()))
+    lib = _native.load()
+    _native.check(lib.cbn_debug_flag_timeout(plan.handle), "flag")
+    with pytest.raises(_native.NativeError, match="timed out"):
+        bn.infer("X19", ev, N_max=32)
+    b, _ = bn.infer("X19", ev, N_max=32)  # cleared
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+def test_out_argument_is_validated(gpu):
+    data, cols, edges = chain_data(6, 4, 3000, 5, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = _t(sample_evidence(data, cols, ["X4"], 100, 3), gpu)
+    bn.infer("X5", ev, N_max=4)
+    good = torch.empty((100, 4), device=gpu)
+    r, _ = bn.engine.infer("X5", ev, 4, out=good)
+    assert r.data_ptr() == good.data_ptr()
+    for bad in (torch.empty((99, 4), device=gpu), torch.empty((100, 4), device=gpu, dtype=torch.float64),
+                torch.empty((4, 100), device=gpu).t()):
+        with pytest.raises((ValueError, RuntimeError)):
+            bn.engine.infer("X5", ev, 4, out=bad)
+
+
+@pytest.mark.parametrize("every", [1, 3])
+def test_stepper_gather_one_rank(every, gpu):
+    """The reassembly path of the stepper over a one-rank RCCL communicator:
+    the returned full tensor equals infer on the batch, for partial groups and
+    an empty batch in the stream."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper
+
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    sizes = [5000, 0, 777, 65536, 1]
+    batches = [_t(sample_evidence(data, cols, names, q, 60 + i), gpu) for i, q in enumerate(sizes)]
+    refs = [bn.infer("X19", b, N_max=32)[0].clone() if q else None for b, q in zip(batches, sizes)]
+    st = ShardedStepper(bn, "X19", 32, exchange_every=every, force_exchange=True, gather=True)
+    outs = [st.step(b)[0] for b in batches]
+    st.wait()
+    torch.cuda.synchronize()
+    for o, r, q in zip(outs, refs, sizes):
+        assert o.shape == (q, 32)
+        if q:
+            np.testing.assert_array_equal(o.cpu().numpy(), r.cpu().numpy())
+    st.close()
