@@ -351,6 +351,27 @@ k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ 
 
 // ---------------------------------------------------------------- query ----
 // Per-factor record staged in LDS for the query prologue.
+// Prefix merge (staged plans): the reference's product starts from ones, so
+// 1 * x_0 = x_0 exactly and the first factors of a query-independent prefix
+// (1-row tables: roots, unobserved-parent factors) fold EXACTLY into the first
+// multi-row factor's table: T_k'[r][j] = (((x_0[j] * x_1[j]) ...) * T_k[r][j])
+// in the reference's order -- the value the query kernel would hold after
+// factor k.  The staged kernel then starts at factor k (fewer LDS row reads).
+// offs: table offsets of factors 0..k (k <= 8).
+struct PrefixOffs {
+    int off[9];
+};
+__global__ void __launch_bounds__(256) k_merge_prefix(float* __restrict__ image, PrefixOffs po, int k, int rows, int N,
+                                                        int RS) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * N) return;
+    const int r = e / N, j = e % N;
+    float v = image[po.off[0] + j];
+    for (int i = 1; i < k; ++i) v = v * image[po.off[i] + j];
+    float* t = image + po.off[k] + (long long)r * RS + j;
+    *t = v * *t;
+}
+
 constexpr int kFqInts = 4 + 2 * kMaxP;  // img_off, kind, n_obs, pad, obs_slot[], obs_card[]
 constexpr int kUnroll = 4;
 
@@ -961,7 +982,8 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int T = (nf + 2) >> 1;  // steps: slots 0 .. 2T-1 cover factors 0 .. nf-1 for both orders
-    const int nsl = 2 * T;        // offset slots per query
+    const int S = (T + 1) >> 1;   // step pairs (one int4 of offsets each)
+    const int nsl = 4 * S;        // offset slots per query (past the last factor: ones rows)
     int* offs = reinterpret_cast<int*>(simg + image_floats);  // [2][kSR][nsl]
     float* wmax = reinterpret_cast<float*>(offs + 2 * kSR * nsl);
     const int tid = threadIdx.x;
@@ -1130,44 +1152,40 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         // step t: slots 2t, 2t + 1 -> four row reads (16 B each: this lane's two
         // column blocks of two rows); step t + 1's reads are in flight while
         // step t is multiplied
-        // all of the query's offsets first (slot pairs, <= 17 steps), so no row
-        // read waits on an offset read
-        int2 ov[17];
-#pragma unroll
-        for (int j = 0; j < 17; ++j)
-            if (j < T) ov[j] = *reinterpret_cast<const int2*>(my + 2 * j);
-        auto load_step = [&](int t, float4& r0, float4& r1, float4& r2, float4& r3) {
-            const int2 o = ov[t];  // t is a compile-time index (the step loop is unrolled)
-            r0 = *reinterpret_cast<const float4*>(simg + o.x + clo);
-            r1 = *reinterpret_cast<const float4*>(simg + o.x + chi);
-            r2 = *reinterpret_cast<const float4*>(simg + o.y + clo);
-            r3 = *reinterpret_cast<const float4*>(simg + o.y + chi);
-        };
+        // step pairs: one int4 of offsets = slots 4sp .. 4sp+3 = steps 2sp, 2sp+1,
+        // each step four row reads (16 B each: this lane's two column blocks of
+        // two rows).  The next pair's offsets are read one pair ahead and each
+        // step's rows are issued while the other step of the pair is multiplied.
         auto mul_step = [&](const float4& r0, const float4& r1, const float4& r2, const float4& r3) {
             acc[0] *= r0.x; acc[1] *= r0.y; acc[2] *= r0.z; acc[3] *= r0.w;
             acc[4] *= r1.x; acc[5] *= r1.y; acc[6] *= r1.z; acc[7] *= r1.w;
             acc[0] *= r2.x; acc[1] *= r2.y; acc[2] *= r2.z; acc[3] *= r2.w;
             acc[4] *= r3.x; acc[5] *= r3.y; acc[6] *= r3.z; acc[7] *= r3.w;
         };
-        // ring of kPD steps: the reads of steps t+1 .. t+kPD-1 are in flight
-        // while step t is multiplied
-        constexpr int kPD = MODE == kModeFused ? 3 : 2;  // (multi-round modes also hold the next round's evidence)
-        float4 rb[kPD][4];
-        load_step(0, rb[0][0], rb[0][1], rb[0][2], rb[0][3]);
-        if (T > 1) load_step(1, rb[1][0], rb[1][1], rb[1][2], rb[1][3]);
+        auto load_step = [&](int oa, int ob, float4& r0, float4& r1, float4& r2, float4& r3) {
+            r0 = *reinterpret_cast<const float4*>(simg + oa + clo);
+            r1 = *reinterpret_cast<const float4*>(simg + oa + chi);
+            r2 = *reinterpret_cast<const float4*>(simg + ob + clo);
+            r3 = *reinterpret_cast<const float4*>(simg + ob + chi);
+        };
+        float4 A0, A1, A2, A3, B0, B1, B2, B3;
+        int4 on = *reinterpret_cast<const int4*>(my);
+        load_step(on.x, on.y, A0, A1, A2, A3);
+        load_step(on.z, on.w, B0, B1, B2, B3);
+        if (S > 1) on = *reinterpret_cast<const int4*>(my + 4);
         CBN_STAMP(4);
 #ifdef CBN_ABL_NOPROD
-        if (T > 0) mul_step(rb[0][0], rb[0][1], rb[0][2], rb[0][3]);
+        mul_step(A0, A1, A2, A3);
 #else
-#pragma unroll
-        for (int t = 0; t < 17; ++t) {
-            if (t < T) {  // wave-uniform
-                if (t + kPD - 1 < T && t + kPD - 1 < 17) {
-                    float4* n = rb[(t + kPD - 1) % kPD];
-                    load_step(t + kPD - 1 < 17 ? t + kPD - 1 : 16, n[0], n[1], n[2], n[3]);
-                }
-                const float4* c = rb[t % kPD];
-                mul_step(c[0], c[1], c[2], c[3]);
+#pragma unroll 1
+        for (int sp = 0; sp < S; ++sp) {  // wave-uniform
+            mul_step(A0, A1, A2, A3);
+            const bool more = sp + 1 < S;
+            if (more) load_step(on.x, on.y, A0, A1, A2, A3);
+            mul_step(B0, B1, B2, B3);
+            if (more) {
+                load_step(on.z, on.w, B0, B1, B2, B3);
+                if (sp + 2 < S) on = *reinterpret_cast<const int4*>(my + 4 * (sp + 2));
             }
         }
 #endif
@@ -1330,11 +1348,14 @@ namespace {
 
 // this call's column pointer of every (factor, observed parent)
 template <int NP>
-FPtrsT<NP> fast_ptrs(const cbn_plan* p, const EvPtrs& ev) {
+FPtrsT<NP> fast_ptrs(const cbn_plan* p, const EvPtrs& ev, int first_factor = 0) {
     FPtrsT<NP> fp;
     // dummy for factors with no observed parent: any column of >= 1 row
     const float* dummy = p->ns > 0 ? ev.p[0] : p->d_image;
-    for (int i = 0; i < NP; ++i) fp.p[i] = p->fast_slot[i] >= 0 ? ev.p[p->fast_slot[i]] : nullptr;
+    for (int i = 0; i < NP; ++i) {
+        const int j = i + first_factor * kFastObs;  // factors from first_factor on
+        fp.p[i] = j < kFastPtrs && p->fast_slot[j] >= 0 ? ev.p[p->fast_slot[j]] : nullptr;
+    }
     for (int f = 0; f < NP / kFastObs; ++f) {
         uintptr_t v = reinterpret_cast<uintptr_t>(fp.p[f * kFastObs]);
         if (!v) v = reinterpret_cast<uintptr_t>(dummy) | kTagNone;
@@ -1358,10 +1379,11 @@ template <int VPL, bool LDS, int MODE>
 void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
                    unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
     if (p->staged) {  // paired N = 32 layout in LDS: the staged kernel (same grid, same words)
+        // factors [prefix, nf): the prefix is folded into factor `prefix`'s table
         hipLaunchKernelGGL((k_query_staged<MODE>), dim3(blocks), dim3(kQueryThreads), p->staged_lds_bytes, s,
-                           p->d_image, p->image_floats, p->rec_off, p->nf, p->zero_off, Q, (Q + blocks - 1) / blocks,
-                           p->d_sync,
-                           epoch, max_in, n_max, max_out, out, fast_ptrs<kFastPtrsSmall>(p, ev));
+                           p->d_image, p->image_floats, p->rec_off + p->prefix * kRecFloats, p->nf - p->prefix,
+                           p->zero_off, Q, (Q + blocks - 1) / blocks, p->d_sync, epoch, max_in, n_max, max_out, out,
+                           fast_ptrs<kFastPtrsSmall>(p, ev, p->prefix));
         return;
     }
     if (p->nf * kFastObs <= kFastPtrsSmall)
@@ -1614,8 +1636,21 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 rows = std::min(rows * factors[f].parent_card[p], 1LL << 40);
         class_rows[f & 1] += rows;
     }
-    const bool paired = vec == 4 && N == 32 && !global_tables && want_vpl >= 2 && !getenv("CBN_NO_PAIRED") &&
-                        std::max(class_rows[0], class_rows[1]) * 64 * 4 <= (long long)kLdsBudget * 3 / 4;
+    bool paired = vec == 4 && N == 32 && !global_tables && want_vpl >= 2 && !getenv("CBN_NO_PAIRED") &&
+                  std::max(class_rows[0], class_rows[1]) * 64 * 4 <= (long long)kLdsBudget * 3 / 4;
+    // leading 1-row factors (roots / unobserved-parent factors) fold into the
+    // first multi-row factor (k_merge_prefix); the staged kernel skips them
+    int prefix = 0;
+    if (paired && !getenv("CBN_NO_PREFIX")) {
+        while (prefix < n_factors - 1 && prefix < 8) {
+            long long rows = 1;
+            for (int p = 0; p < factors[prefix].n_parents && p < kMaxP; ++p)
+                if (factors[prefix].parent_ev_slot[p] >= 0 && factors[prefix].parent_card[p] > 0)
+                    rows *= factors[prefix].parent_card[p];
+            if (rows != 1) break;
+            ++prefix;
+        }
+    }
     const int RS = paired ? 64 : vec == 4 && !global_tables ? N + 4 : N;
     const long long talign = global_tables ? 32 : 4;
     long long class_start[2] = {0, 0};
@@ -1678,8 +1713,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         const long long F_eff = h.kind == CBN_FACTOR_SCALAR ? N : F;
         d.wave_mode = F_eff >= kWave ? 1 : 0;
         if (paired) {
-            d.table_off = (int)(class_start[f & 1] * 64 + (f & 1) * 32);
-            class_start[f & 1] += rows;
+            // bank half by the index the staged kernel sees (prefix factors: half 0, never read there)
+            const int c = f < prefix ? 0 : (f - prefix) & 1;
+            d.table_off = (int)(class_start[c] * 64 + c * 32);
+            class_start[c] += rows;
             off = std::max(class_start[0], class_start[1]) * 64;
         } else {
             d.table_off = (int)off;
@@ -1719,6 +1756,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->image_floats = (int)off;
     P->table_floats = (int)table_floats;
     P->zero_off = (int)zero_off;
+    P->prefix = prefix;
+    for (int i = 0; i <= prefix && i < 9; ++i) P->prefix_offs[i] = fac[i].table_off;
+    P->prefix_rows = prefix > 0 ? fac[prefix].rows : 0;
     P->rec_off = (int)rec_off;
     P->RS = RS;
     // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
@@ -1829,8 +1869,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             P->fast = true;
             P->vpl = vpl;
             P->paired = paired && vpl == 2 && P->use_lds;
-            const size_t st_bytes = img_bytes + (size_t)2 * kSR * (n_factors + 2) * 4 + (kQueryThreads / kWave) * 4 + 64;
-            if (P->paired && n_factors * kFastObs <= kFastPtrsSmall && st_bytes <= (size_t)kLdsBudget &&
+            const size_t st_bytes = img_bytes + (size_t)2 * kSR * (n_factors + 4) * 4 + (kQueryThreads / kWave) * 4 + 64;
+            if (P->paired && (n_factors - P->prefix) * kFastObs <= kFastPtrsSmall && st_bytes <= (size_t)kLdsBudget &&
                 !getenv("CBN_NO_STAGED")) {
                 P->staged = true;
                 P->staged_lds_bytes = (st_bytes + 15) & ~size_t(15);
@@ -1866,6 +1906,12 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                     P->fused_ok = true;
             }
         }
+    }
+    if (!P->staged && P->prefix) {
+        // the merge is only valid for the staged kernel (the others multiply every
+        // factor): a non-staged plan with a paired layout keeps its tables as built
+        P->prefix = 0;
+        P->prefix_rows = 0;
     }
     allow_lds<4, true, false>(kLdsBudget); allow_lds<4, true, true>(kLdsBudget);
     allow_lds<1, true, false>(kLdsBudget); allow_lds<1, true, true>(kLdsBudget);
@@ -1912,6 +1958,14 @@ int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
     hipLaunchKernelGGL(k_build_tables, dim3((unsigned)blocks), dim3(kBuildThreads), 0, s, plan->d_fac,
                        plan->d_build, plan->n_build, plan->build_units, plan->N, plan->RS, plan->d_image);
     HIP_TRY(hipGetLastError());
+    if (plan->prefix > 0) {
+        PrefixOffs po;
+        for (int i = 0; i < 9; ++i) po.off[i] = plan->prefix_offs[i];
+        const int n = plan->prefix_rows * plan->N;
+        hipLaunchKernelGGL(k_merge_prefix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, plan->d_image, po,
+                           plan->prefix, plan->prefix_rows, plan->N, plan->RS);
+        HIP_TRY(hipGetLastError());
+    }
     return CBN_OK;
 }
 

@@ -77,6 +77,9 @@ struct cbn_plan {
     bool staged = false;         // paired plans of <= 32 factors: k_query_staged (evidence staged by factor)
     size_t staged_lds_bytes = 0;
     int zero_off = -1;
+    int prefix = 0;              // staged plans: leading 1-row factors folded into factor `prefix` (k_merge_prefix)
+    int prefix_offs[9] = {};     // table offsets of factors 0..prefix
+    int prefix_rows = 0;         // rows of factor `prefix`'s table
     unsigned* h_status = nullptr;  // host-mapped: 1 after a fused launch timed out (reported by the next run)           // paired layout: float offset of the zero super-row (ones super-row at +64)
     unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
