@@ -16,8 +16,9 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 CBN_MAX_PARENTS = 8
+CBN_MAX_DIRECT_PARENTS = 32
 CBN_MAX_EVIDENCE = 256
 CBN_FACTOR_SCALAR = 0
 CBN_FACTOR_SHARED = 1
@@ -77,6 +78,33 @@ class ParamFactor(ctypes.Structure):
     ]
 
 
+class CpdRef(ctypes.Structure):
+    """Mirror of ``cbn_cpd_ref`` (include/cbn_amd.h)."""
+
+    _fields_ = [
+        ("n_cols", ctypes.c_int32),
+        ("domains", ctypes.POINTER(ctypes.c_void_p)),
+        ("cards", _c_int_p),
+        ("dense", ctypes.c_void_p),
+        ("keys", ctypes.c_void_p),
+        ("vals", ctypes.c_void_p),
+        ("capacity", ctypes.c_int64),
+    ]
+
+
+class DirectFactor(ctypes.Structure):
+    """Mirror of ``cbn_direct_factor`` (include/cbn_amd.h)."""
+
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("n_parents", ctypes.c_int32),
+        ("parent_ev_slot", _c_int_p),
+        ("node_sample_idx", ctypes.c_void_p),
+        ("parent_sample_idx", ctypes.c_void_p),
+        ("cpd", CpdRef),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "cbn_abi_version": (ctypes.c_int, []),
@@ -113,15 +141,22 @@ _SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_void_p)]),
     "cbn_param_eval": (ctypes.c_int, [ctypes.POINTER(ParamModel), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbn_hash_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "cbn_cpd_ref_eval": (ctypes.c_int, [ctypes.POINTER(CpdRef), ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    "cbn_plan_create_direct": (ctypes.c_int, [ctypes.POINTER(DirectFactor), ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.POINTER(ctypes.c_void_p)]),
 }
 CBN_RUN_BUILD_TABLES = 1
 CBN_RUN_TIMED = 2
 CBN_RUN_TWO_PASS = 4
 CBN_RUN_RAW = 8
+CBN_E_LIMIT = -3
 CBN_E_UNSUPPORTED = -4
 CBN_E_TIMEOUT = -5
 CBN_PLAN_FAST, CBN_PLAN_LDS, CBN_PLAN_PAIRED, CBN_PLAN_STAGED = 1, 2, 4, 8
-CBN_PLAN_FUSED, CBN_PLAN_PARAMETRIC, CBN_PLAN_VPL2 = 16, 32, 64
+CBN_PLAN_FUSED, CBN_PLAN_PARAMETRIC, CBN_PLAN_VPL2, CBN_PLAN_DIRECT = 16, 32, 64, 128
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

@@ -1,0 +1,467 @@
+// cbn_direct.hip -- direct-evaluation inference plans and hashed BruteForce
+// CPDs (gfx950).
+//
+// Reference: BayesianNetwork.infer (cbn/base/bayesian_network.py:208-305) over
+// factors from Node.get_prob (cbn/base/node.py:115-204) evaluated by
+// BruteForce._get_prob (cbn/parameter_learning/brute_force.py:185-257), which
+// answers ANY fitted data -- continuous or high-cardinality columns, any
+// number of parents -- with equality scans over the unique training rows.
+//
+// The table path (cbn_infer.hip) tabulates every factor over its observed
+// parents' domains: prod(observed cards) rows x N.  For ~1 000-value columns
+// or nodes with many parents that is unbounded, so a DIRECT plan evaluates
+// each factor per (query, sample column) from the CPD itself -- a dense array
+// when it fits, else a hash table of the unique rows (key = mixed-radix domain
+// index, value = joint / (parent marginal + 1e-10), built at fit):
+//   x_f[q, j] = (1 / F) sum over free-parent sample combos c of
+//               P(node = s_j | observed parents = e_q, free parents = c)
+// with F = N^(free parents) (node.py:152-193 + torch.mean of
+// bayesian_network.py:292), multiplied into the row in the reference's
+// factor order; roots and no-observed-parent factors are query-independent
+// constants computed once per plan (k_direct_const).  One raw launch (rows +
+// one max word per block), then k_scale divides by the global max -- the same
+// two steps the sharded path runs around its all-reduce.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "cbn_internal.h"
+
+using namespace cbn;
+
+namespace cbn {
+
+constexpr int kMaxDP = CBN_MAX_DIRECT_PARENTS;
+
+struct DevCpd {
+    const float* dense;      // dense CPD (or nullptr)
+    const long long* keys;   // hash table keys (-1: empty)
+    const float* vals;
+    long long mask;          // capacity - 1
+};
+
+struct DevDCol {             // one parent column of a direct factor
+    const float* dom;        // sorted domain (observed parents)
+    const int* sample_idx;   // [N] free-parent sample -> domain idx (-1: none)
+    long long stride;        // mixed-radix weight of this column
+    int card;
+    int ev_slot;             // evidence column or -1 (free)
+};
+
+struct DevDirect {
+    int kind;
+    int n_parents;
+    int n_obs;
+    int n_free;
+    long long free_combos;   // N^n_free
+    const int* node_sample_idx;
+    DevCpd cpd;
+    int cidx;                // constant factors: row of the plan's const buffer
+    int pad;
+    DevDCol col[kMaxDP];
+};
+
+struct DirectPlan {
+    int nf = 0;
+    int ns = 0;
+    int N = 0;
+    DevDirect* d_fac = nullptr;
+    float* d_const = nullptr;   // [n_const][N]: SCALAR (replicated) / SHARED rows
+    int* d_cfac = nullptr;      // [n_const]: factor of each const row
+    int n_const = 0;
+    int max_slots = 0;
+};
+
+}  // namespace cbn
+
+namespace {
+
+#define DHIP_TRY(expr)                                                                    \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return set_err(CBN_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));     \
+    } while (0)
+
+constexpr int kDThreads = 256;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31;
+    return x;
+}
+
+__device__ __forceinline__ float hash_get(const long long* __restrict__ keys, const float* __restrict__ vals,
+                                          long long mask, long long key) {
+    long long h = (long long)(mix64((unsigned long long)key) & (unsigned long long)mask);
+    for (long long probe = 0; probe <= mask; ++probe) {
+        const long long k = keys[h];
+        if (k == key) return vals[h];
+        if (k < 0) return 0.f;
+        h = (h + 1) & mask;
+    }
+    return 0.f;
+}
+
+__device__ __forceinline__ float cpd_get(const DevCpd& c, long long key) {
+    return c.dense ? c.dense[key] : hash_get(c.keys, c.vals, c.mask, key);
+}
+
+__device__ __forceinline__ int bsearch_dom(const float* __restrict__ dom, int card, float x) {
+    int lo = 0, hi = card;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (dom[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return (lo < card && dom[lo] == x) ? lo : -1;
+}
+
+__global__ void k_hash_clear(long long* __restrict__ keys, float* __restrict__ vals, long long cap) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < cap; i += (long long)gridDim.x * blockDim.x) {
+        keys[i] = -1;
+        vals[i] = 0.f;
+    }
+}
+
+__global__ void k_hash_insert(const long long* __restrict__ in_keys, const float* __restrict__ in_vals, long long n,
+                              long long* __restrict__ keys, float* __restrict__ vals, long long mask) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long key = in_keys[i];
+        long long h = (long long)(mix64((unsigned long long)key) & (unsigned long long)mask);
+        for (long long probe = 0; probe <= mask; ++probe) {
+            const unsigned long long prev =
+                atomicCAS(reinterpret_cast<unsigned long long*>(keys + h), ~0ULL, (unsigned long long)key);
+            if (prev == ~0ULL || prev == (unsigned long long)key) {
+                vals[h] = in_vals[i];
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
+}
+
+struct RefCols {
+    const float* dom[kMaxDP + 1];
+    int card[kMaxDP + 1];
+    long long stride[kMaxDP + 1];
+};
+
+__global__ void k_cpd_ref_eval(DevCpd c, int n_cols, RefCols rc, const float* __restrict__ pts, long long n,
+                               float* __restrict__ out) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        long long key = 0;
+        bool ok = true;
+        for (int k = 0; k < n_cols; ++k) {
+            const int idx = bsearch_dom(rc.dom[k], rc.card[k], pts[i * n_cols + k]);
+            ok &= idx >= 0;
+            key += (long long)(idx < 0 ? 0 : idx) * rc.stride[k];
+        }
+        out[i] = ok ? cpd_get(c, key) : 0.f;
+    }
+}
+
+// x_f[j] for query-independent factors (SCALAR: mean over the N node
+// samples, replicated; SHARED: mean over the N^k parent sample combos)
+__device__ float direct_free_mean(const DevDirect& d, long long base, int N) {
+    float s = 0.f;
+    for (long long c = 0; c < d.free_combos; ++c) {
+        long long key = base, cc = c;
+        bool ok = true;
+        for (int p = d.n_parents - 1; p >= 0; --p) {
+            const DevDCol& col = d.col[p];
+            if (col.ev_slot < 0) {
+                const long long qq = cc / N;
+                const int pi = col.sample_idx[cc - qq * N];
+                cc = qq;
+                ok &= pi >= 0;
+                key += (long long)(pi < 0 ? 0 : pi) * col.stride;
+            }
+        }
+        s += ok ? cpd_get(d.cpd, key) : 0.f;
+    }
+    return s;
+}
+
+__global__ void k_direct_const(const DevDirect* __restrict__ fac, const int* __restrict__ cfac, int n_const, int N,
+                               float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_const * N) return;
+    const int r = i / N, j = i - r * N;
+    const DevDirect& d = fac[cfac[r]];
+    float x;
+    if (d.kind == CBN_FACTOR_SCALAR) {
+        float s = 0.f;
+        for (int jj = 0; jj < N; ++jj) {
+            const int ni = d.node_sample_idx[jj];
+            s += ni >= 0 ? cpd_get(d.cpd, ni) : 0.f;
+        }
+        x = s / (float)N;
+    } else {
+        const int ni = d.node_sample_idx[j];
+        x = ni < 0 ? 0.f : direct_free_mean(d, ni, N) / (float)d.free_combos;
+    }
+    out[i] = x;
+}
+
+struct DEv {
+    const float* p[CBN_MAX_EVIDENCE];
+};
+
+// one thread per (query, sample column): the product over factors in the
+// reference's order; unnormalised rows + one max word per block
+__global__ void __launch_bounds__(kDThreads) k_query_direct(const DevDirect* __restrict__ fac, int nf, int N,
+                                                             const float* __restrict__ cst, DEv ev, long long Q,
+                                                             unsigned* __restrict__ words, int n_words,
+                                                             float* __restrict__ out) {
+    const long long n = Q * N;
+    unsigned lmaxb = 0;
+    for (long long it = blockIdx.x * (long long)blockDim.x + threadIdx.x; it < n;
+         it += (long long)gridDim.x * blockDim.x) {
+        const long long q = it / N;
+        const int j = (int)(it - q * N);
+        float acc = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        for (int f = 0; f < nf; ++f) {
+            const DevDirect& d = fac[f];
+            float x;
+            if (d.kind != CBN_FACTOR_QUERY) {
+                x = cst[(long long)d.cidx * N + j];
+            } else {
+                const int ni = d.node_sample_idx[j];
+                long long base = ni < 0 ? 0 : ni;
+                bool ok = ni >= 0;
+                for (int p = 0; p < d.n_parents; ++p) {
+                    const DevDCol& col = d.col[p];
+                    if (col.ev_slot >= 0) {
+                        const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
+                        ok &= idx >= 0;
+                        base += (long long)(idx < 0 ? 0 : idx) * col.stride;
+                    }
+                }
+                x = ok ? direct_free_mean(d, base, N) / (float)d.free_combos : 0.f;
+            }
+            acc = acc * x;
+        }
+        out[it] = acc;
+        // non-negative floats: unsigned order == float order, and NaN bits sort
+        // above +inf -- a NaN row makes the max NaN, as torch.max does
+        lmaxb = max(lmaxb, __float_as_uint(acc));
+    }
+    // block max -> one word
+    __shared__ unsigned wm[kDThreads / kWave];
+    unsigned m = lmaxb;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, kWave));
+    if ((threadIdx.x & (kWave - 1)) == 0) wm[threadIdx.x / kWave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned b = 0;
+        for (int i = 0; i < kDThreads / kWave; ++i) b = max(b, wm[i]);
+        words[blockIdx.x] = b;
+    }
+    if (blockIdx.x == 0)
+        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += blockDim.x) words[i] = 0u;
+}
+
+int fill_cols(const cbn_cpd_ref& r, long long* stride, const char* what, int f) {
+    if (r.n_cols < 1 || r.n_cols > kMaxDP + 1 || !r.domains || !r.cards)
+        return set_err(CBN_E_ARG, "%s %d: bad CPD columns", what, f);
+    if (!r.dense && (!r.keys || !r.vals || r.capacity < 2 || (r.capacity & (r.capacity - 1))))
+        return set_err(CBN_E_ARG, "%s %d: CPD is neither dense nor a power-of-two hash table", what, f);
+    long long s = 1;
+    for (int k = r.n_cols - 1; k >= 0; --k) {
+        if (r.cards[k] <= 0 || !r.domains[k]) return set_err(CBN_E_ARG, "%s %d: column %d domain", what, f, k);
+        stride[k] = s;
+        if (s > (1LL << 62) / r.cards[k]) return set_err(CBN_E_LIMIT, "%s %d: prod(cards) >= 2^62", what, f);
+        s *= r.cards[k];
+    }
+    return CBN_OK;
+}
+
+DevCpd dev_cpd(const cbn_cpd_ref& r) {
+    DevCpd c;
+    c.dense = r.dense;
+    c.keys = reinterpret_cast<const long long*>(r.keys);
+    c.vals = r.vals;
+    c.mask = r.dense ? 0 : r.capacity - 1;
+    return c;
+}
+
+}  // namespace
+
+void cbn::direct_destroy(DirectPlan* dp) {
+    if (!dp) return;
+    if (dp->d_fac) (void)hipFree(dp->d_fac);
+    if (dp->d_const) (void)hipFree(dp->d_const);
+    if (dp->d_cfac) (void)hipFree(dp->d_cfac);
+    delete dp;
+}
+
+int cbn::direct_max_words(const DirectPlan* dp) { return dp ? dp->max_slots : 0; }
+
+int cbn::direct_build_consts(DirectPlan* dp, hipStream_t s) {
+    if (!dp || dp->n_const == 0) return CBN_OK;
+    const int n = dp->n_const * dp->N;
+    hipLaunchKernelGGL(k_direct_const, dim3((n + 255) / 256), dim3(256), 0, s, dp->d_fac, dp->d_cfac, dp->n_const,
+                       dp->N, dp->d_const);
+    DHIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+int cbn::direct_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+                    uint32_t* max_bits, float* out, int32_t flags, hipStream_t s) {
+    DirectPlan* dp = plan->direct;
+    if (n_evidence != dp->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", dp->ns, n_evidence);
+    if (n_queries <= 0) return set_err(CBN_E_ARG, "cbn_plan_run: direct plans need >= 1 query");
+    if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
+    DEv ev;
+    memset(&ev, 0, sizeof(ev));
+    for (int i = 0; i < n_evidence; ++i) {
+        if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+        ev.p[i] = evidence[i];
+    }
+    if (flags & CBN_RUN_BUILD_TABLES) {
+        const int rc = direct_build_consts(dp, s);
+        if (rc) return rc;
+    }
+    const long long n = n_queries * (long long)dp->N;
+    long long grid = (n + kDThreads - 1) / kDThreads;
+    grid = std::max(1LL, std::min(grid, (long long)dp->max_slots));
+    const bool raw = (flags & CBN_RUN_RAW) != 0;
+    unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
+    hipLaunchKernelGGL(k_query_direct, dim3((unsigned)grid), dim3(kDThreads), 0, s, dp->d_fac, dp->nf, dp->N,
+                       dp->d_const, ev, (long long)n_queries, words, dp->max_slots, out);
+    DHIP_TRY(hipGetLastError());
+    if (raw) return CBN_OK;
+    if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_plan_run: out must be 16-B aligned");
+    return launch_scale(out, n, words, dp->max_slots, max_bits, s);
+}
+
+extern "C" {
+
+int cbn_hash_build(const int64_t* keys, const float* vals, int64_t n, int64_t* table_keys, float* table_vals,
+                   int64_t capacity, void* stream) {
+    if (n < 0 || capacity < 2 || (capacity & (capacity - 1)) || n > capacity / 2 || !table_keys || !table_vals ||
+        (n > 0 && (!keys || !vals)))
+        return set_err(CBN_E_ARG, "cbn_hash_build: bad arguments (capacity a power of two >= 2 n)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const long long gc = std::min<long long>((capacity + 255) / 256, 4LL * num_cu());
+    hipLaunchKernelGGL(k_hash_clear, dim3((unsigned)gc), dim3(256), 0, s, reinterpret_cast<long long*>(table_keys),
+                       table_vals, (long long)capacity);
+    DHIP_TRY(hipGetLastError());
+    if (n == 0) return CBN_OK;
+    const long long gi = std::min<long long>((n + 255) / 256, 4LL * num_cu());
+    hipLaunchKernelGGL(k_hash_insert, dim3((unsigned)gi), dim3(256), 0, s, reinterpret_cast<const long long*>(keys),
+                       vals, (long long)n, reinterpret_cast<long long*>(table_keys), table_vals,
+                       (long long)(capacity - 1));
+    DHIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+int cbn_cpd_ref_eval(const cbn_cpd_ref* cpd, const float* points, int64_t n_points, float* out, void* stream) {
+    if (!cpd || n_points < 0 || (n_points > 0 && (!points || !out))) return set_err(CBN_E_ARG, "cbn_cpd_ref_eval: bad arguments");
+    RefCols rc;
+    memset(&rc, 0, sizeof(rc));
+    int e = fill_cols(*cpd, rc.stride, "cpd", 0);
+    if (e) return e;
+    for (int k = 0; k < cpd->n_cols; ++k) {
+        rc.dom[k] = cpd->domains[k];
+        rc.card[k] = cpd->cards[k];
+    }
+    if (n_points == 0) return CBN_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const long long g = std::min<long long>((n_points + 255) / 256, 4LL * num_cu());
+    hipLaunchKernelGGL(k_cpd_ref_eval, dim3((unsigned)g), dim3(256), 0, s, dev_cpd(*cpd), cpd->n_cols, rc, points,
+                       (long long)n_points, out);
+    DHIP_TRY(hipGetLastError());
+    return CBN_OK;
+}
+
+int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, int32_t n_samples, cbn_plan** plan) {
+    if (!plan || !factors || n_factors <= 0 || n_samples <= 0)
+        return set_err(CBN_E_ARG, "cbn_plan_create_direct: bad arguments");
+    *plan = nullptr;
+    const int N = n_samples;
+    std::vector<DevDirect> host(n_factors);
+    int ns = 0, n_const = 0;
+    for (int f = 0; f < n_factors; ++f) {
+        const cbn_direct_factor& h = factors[f];
+        DevDirect& d = host[f];
+        memset(&d, 0, sizeof(d));
+        if (h.kind < CBN_FACTOR_SCALAR || h.kind > CBN_FACTOR_QUERY)
+            return set_err(CBN_E_ARG, "factor %d: bad kind %d", f, h.kind);
+        if (h.n_parents < 0 || h.n_parents > kMaxDP)
+            return set_err(CBN_E_LIMIT, "factor %d: %d parents > %d", f, h.n_parents, kMaxDP);
+        if ((h.kind == CBN_FACTOR_SCALAR) != (h.n_parents == 0)) return set_err(CBN_E_ARG, "factor %d: SCALAR iff root", f);
+        if (!h.node_sample_idx) return set_err(CBN_E_ARG, "factor %d: missing node samples", f);
+        if (h.cpd.n_cols != h.n_parents + 1) return set_err(CBN_E_ARG, "factor %d: CPD has %d columns", f, h.cpd.n_cols);
+        long long stride[kMaxDP + 1];
+        int e = fill_cols(h.cpd, stride, "factor", f);
+        if (e) return e;
+        d.kind = h.kind;
+        d.n_parents = h.n_parents;
+        d.node_sample_idx = h.node_sample_idx;
+        d.cpd = dev_cpd(h.cpd);
+        long long F = 1;
+        for (int p = 0; p < h.n_parents; ++p) {
+            DevDCol& c = d.col[p];
+            c.dom = h.cpd.domains[p];
+            c.card = h.cpd.cards[p];
+            c.stride = stride[p];
+            c.ev_slot = h.parent_ev_slot ? h.parent_ev_slot[p] : -1;
+            if (c.ev_slot >= CBN_MAX_EVIDENCE) return set_err(CBN_E_ARG, "factor %d: evidence slot %d", f, c.ev_slot);
+            if (c.ev_slot >= 0) {
+                ++d.n_obs;
+                ns = std::max(ns, c.ev_slot + 1);
+            } else {
+                if (!h.parent_sample_idx) return set_err(CBN_E_ARG, "factor %d: free parent without samples", f);
+                c.sample_idx = h.parent_sample_idx + (long long)p * N;
+                ++d.n_free;
+                if (F > (1LL << 40) / N) return set_err(CBN_E_LIMIT, "factor %d: too many free-parent combos", f);
+                F *= N;
+            }
+        }
+        d.free_combos = F;
+        if ((h.kind == CBN_FACTOR_QUERY) != (d.n_obs > 0)) return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
+        if (h.kind != CBN_FACTOR_QUERY) d.cidx = n_const++;
+    }
+    DirectPlan* dp = new DirectPlan();
+    dp->nf = n_factors;
+    dp->ns = ns;
+    dp->N = N;
+    dp->n_const = n_const;
+    dp->max_slots = std::min(4 * num_cu(), kMaxSlots);
+    std::vector<int> cfac;
+    for (int f = 0; f < n_factors; ++f)
+        if (host[f].kind != CBN_FACTOR_QUERY) cfac.push_back(f);
+    cbn_plan* P = new cbn_plan();
+    P->nf = n_factors;
+    P->ns = ns;
+    P->N = N;
+    P->direct = dp;
+    bool ok = hipMalloc(&dp->d_fac, sizeof(DevDirect) * n_factors) == hipSuccess &&
+              hipMalloc(&dp->d_const, sizeof(float) * std::max(1, n_const * N)) == hipSuccess &&
+              hipMalloc(&dp->d_cfac, sizeof(int) * std::max(1, n_const)) == hipSuccess &&
+              hipMalloc(&P->d_sync, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    ok = ok && hipMemcpy(dp->d_fac, host.data(), sizeof(DevDirect) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && (cfac.empty() ||
+                hipMemcpy(dp->d_cfac, cfac.data(), sizeof(int) * cfac.size(), hipMemcpyHostToDevice) == hipSuccess);
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    if (!ok) {
+        cbn_plan_destroy(P);
+        return set_err(CBN_E_HIP, "cbn_plan_create_direct: device allocation/upload failed");
+    }
+    int rc = direct_build_consts(dp, nullptr);
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = set_err(CBN_E_HIP, "cbn_plan_create_direct: const build failed");
+    if (rc) {
+        cbn_plan_destroy(P);
+        return rc;
+    }
+    *plan = P;
+    return CBN_OK;
+}
+
+}  // extern "C"

@@ -1939,6 +1939,7 @@ int cbn_plan_destroy(cbn_plan* plan) {
     if (plan->d_sync) (void)hipFree(plan->d_sync);
     if (plan->h_status) (void)hipHostFree(plan->h_status);
     if (plan->param) param_destroy(plan->param);
+    if (plan->direct) direct_destroy(plan->direct);
     delete plan;
     return CBN_OK;
 }
@@ -1951,6 +1952,7 @@ int cbn_plan_uses_lds(const cbn_plan* plan) { return plan && plan->use_lds ? 1 :
 
 int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
     if (!plan) return set_err(CBN_E_ARG, "null plan");
+    if (plan->direct) return direct_build_consts(plan->direct, reinterpret_cast<hipStream_t>(stream));
     if (plan->build_units == 0) return CBN_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     long long blocks = ((long long)plan->build_units * kWave + kBuildThreads - 1) / kBuildThreads;
@@ -1972,7 +1974,8 @@ int cbn_plan_build_tables(cbn_plan* plan, void* stream) {
 int cbn_plan_query_max(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
                        uint32_t* max_bits, void* stream) {
     if (!plan || !max_bits || n_queries < 0) return set_err(CBN_E_ARG, "cbn_plan_query_max: bad arguments");
-    if (plan->param) return set_err(CBN_E_UNSUPPORTED, "parametric plans run through cbn_plan_run (raw + scale)");
+    if (plan->param || plan->direct)
+        return set_err(CBN_E_UNSUPPORTED, "parametric / direct plans run through cbn_plan_run (raw + scale)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (n_queries == 0) {
         HIP_TRY(hipMemsetAsync(max_bits, 0, sizeof(uint32_t), s));
@@ -1985,7 +1988,8 @@ int cbn_plan_query_write(cbn_plan* plan, int64_t n_queries, const float* const* 
                          const uint32_t* max_bits, float* out, void* stream) {
     if (!plan || !max_bits || n_queries < 0 || (n_queries > 0 && !out))
         return set_err(CBN_E_ARG, "cbn_plan_query_write: bad arguments");
-    if (plan->param) return set_err(CBN_E_UNSUPPORTED, "parametric plans run through cbn_plan_run (raw + scale)");
+    if (plan->param || plan->direct)
+        return set_err(CBN_E_UNSUPPORTED, "parametric / direct plans run through cbn_plan_run (raw + scale)");
     return dispatch_query<true>(plan, n_queries, evidence, n_evidence, const_cast<uint32_t*>(max_bits), out,
                                 reinterpret_cast<hipStream_t>(stream));
 }
@@ -2000,6 +2004,7 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
+    if (plan->direct) return direct_run(plan, n_queries, evidence, n_evidence, max_bits, out, flags, s);
     if (plan->param) {
         hipEvent_t* e = nullptr;
         if ((flags & CBN_RUN_TIMED) && plan->ev_n < cbn_plan::kRing) {
@@ -2151,11 +2156,12 @@ int32_t cbn_plan_flags(const cbn_plan* plan) {
     return (plan->fast ? CBN_PLAN_FAST : 0) | (plan->use_lds ? CBN_PLAN_LDS : 0) |
            (plan->paired ? CBN_PLAN_PAIRED : 0) | (plan->staged ? CBN_PLAN_STAGED : 0) |
            (plan->fused_ok ? CBN_PLAN_FUSED : 0) | (plan->param ? CBN_PLAN_PARAMETRIC : 0) |
-           (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0);
+           (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0) | (plan->direct ? CBN_PLAN_DIRECT : 0);
 }
 
 int32_t cbn_plan_max_words(const cbn_plan* plan) {
     if (plan && plan->param) return param_max_words(plan->param);
+    if (plan && plan->direct) return direct_max_words(plan->direct);
     return plan && plan->fast ? plan->max_slots : 0;
 }
 

@@ -35,6 +35,7 @@ struct DevFactor;
 struct QSlot;
 struct BuildItem;
 struct ParamPlan;  // cbn_param.hip
+struct DirectPlan;  // cbn_direct.hip
 
 int set_err(int code, const char* fmt, ...);
 int num_cu();
@@ -48,6 +49,13 @@ int param_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, i
               uint32_t* max_bits, float* out, int32_t flags, hipStream_t s);
 void param_destroy(ParamPlan* pp);
 int param_max_words(const ParamPlan* pp);
+
+// direct plans (cbn_direct.hip)
+int direct_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+               uint32_t* max_bits, float* out, int32_t flags, hipStream_t s);
+int direct_build_consts(DirectPlan* dp, hipStream_t s);
+void direct_destroy(DirectPlan* dp);
+int direct_max_words(const DirectPlan* dp);
 
 }  // namespace cbn
 
@@ -92,6 +100,7 @@ struct cbn_plan {
     size_t lds_bytes = 0;
     int blocks_per_cu = 1;
     cbn::ParamPlan* param = nullptr;  // parametric-CPD plan (cbn_plan_create_param); table fields unused
+    cbn::DirectPlan* direct = nullptr;  // direct plan (cbn_plan_create_direct); table fields unused
 };
 
 #endif  // CBN_INTERNAL_H

@@ -64,6 +64,7 @@ class Plan:
     keep: list = field(default_factory=list)
     max_bits: Optional[torch.Tensor] = None
     tables_built: bool = False
+    direct: bool = False  # factors evaluated from the CPDs (cbn_plan_create_direct)
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -156,6 +157,10 @@ class InferenceEngine:
         self.fused = True
         self._fast: Dict[tuple, "_FastPath"] = {}
         self._gen = GENERATION[0]  # estimator generation the cached plans were built under
+        # evaluate every BruteForce factor from its CPD (direct plans) even when
+        # the table path could take the plan (tests; the direct path is chosen
+        # by itself for hashed CPDs, > 8 parents and oversized tables)
+        self.force_direct = False
 
     def _check_generation(self):
         """Drop every cached plan when any estimator was refitted / reloaded /
@@ -190,6 +195,11 @@ class InferenceEngine:
         if any(param):
             raise NotImplementedError("a plan mixing BruteForce tables and parametric estimators is not supported "
                                       "(the reference fits one estimator type per network)")
+        for spec in plan.factors:
+            self.bn.nodes_obj[spec.node].estimator.compiled()
+        if self.force_direct or any(self.bn.nodes_obj[s.node].estimator.sparse or len(s.parents) > CBN_MAX_PARENTS
+                                    for s in plan.factors):
+            return self._materialise_direct(plan, device)
         lib = _native.load()
         descs = (_native.FactorDesc * len(plan.factors))()
         keep = []
@@ -205,8 +215,6 @@ class InferenceEngine:
                 d = descs[f]
                 d.kind = spec.kind
                 d.n_parents = len(spec.parents)
-                if d.n_parents > CBN_MAX_PARENTS:
-                    raise _native.NativeError(f"node {spec.node}: {d.n_parents} parents > {CBN_MAX_PARENTS}")
                 d.node_card = int(doms[-1].numel())
                 d.cpd = cpd.data_ptr() if spec.kind != CBN_FACTOR_SCALAR else est.node_marginal.data_ptr()
                 nidx = domain_index(spec.node_samples, doms[-1])
@@ -228,10 +236,70 @@ class InferenceEngine:
                         d.parent_ev_slot[i] = -1
             handle = ctypes.c_void_p()
             torch.cuda.current_stream(device).synchronize()  # index arrays ready before the D2D copies
-            _native.check(lib.cbn_plan_create(descs, len(plan.factors), N, ctypes.byref(handle)),
-                          "cbn_plan_create")
+            rc = lib.cbn_plan_create(descs, len(plan.factors), N, ctypes.byref(handle))
+            if rc == _native.CBN_E_LIMIT:  # factor tables / N beyond the table path: evaluate directly
+                return self._materialise_direct(plan, device)
+            _native.check(rc, "cbn_plan_create")
         plan.handle = handle
         plan.keep = keep
+        plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def _materialise_direct(self, plan: Plan, device: torch.device):
+        """cbn_direct_factor per ancestor (include/cbn_amd.h): each factor is
+        evaluated per (query, sample column) from its CPD -- dense or hashed --
+        with no per-plan table (nodes with > 8 parents, hashed CPDs of
+        continuous / high-cardinality columns, factor tables beyond the
+        table path's limits).  Same sample-index conventions as the table path."""
+        lib = _native.load()
+        descs = (_native.DirectFactor * len(plan.factors))()
+        keep = []
+        slot_of = {v: i for i, v in enumerate(plan.slots)}
+        N = plan.n_samples
+        with torch.cuda.device(device):
+            for f, spec in enumerate(plan.factors):
+                est = self.bn.nodes_obj[spec.node].estimator
+                est.compiled()
+                doms = est.domains
+                k = len(spec.parents)
+                if k > _native.CBN_MAX_DIRECT_PARENTS:
+                    raise _native.NativeError(f"node {spec.node}: {k} parents > {_native.CBN_MAX_DIRECT_PARENTS}")
+                d = descs[f]
+                d.kind = spec.kind
+                d.n_parents = k
+                if spec.kind == CBN_FACTOR_SCALAR:
+                    # root: the node marginal (brute_force.py:205-214) as a one-column dense CPD
+                    mdoms = (ctypes.c_void_p * 1)(doms[-1].data_ptr())
+                    mcards = (ctypes.c_int32 * 1)(int(doms[-1].numel()))
+                    ref = _native.CpdRef()
+                    ref.n_cols = 1
+                    ref.domains = ctypes.cast(mdoms, ctypes.POINTER(ctypes.c_void_p))
+                    ref.cards = ctypes.cast(mcards, ctypes.POINTER(ctypes.c_int32))
+                    ref.dense = est.node_marginal.data_ptr()
+                    host = (mdoms, mcards)
+                else:
+                    ref, host = est.cpd_ref()
+                d.cpd = ref
+                keep += [host, est.cpd, est.hash_keys, est.hash_vals, est.node_marginal, *doms]
+                nidx = domain_index(spec.node_samples, doms[-1])
+                keep.append(nidx)
+                d.node_sample_idx = nidx.data_ptr()
+                if k:
+                    ev = (ctypes.c_int32 * k)(*[slot_of[p] if p in spec.observed else -1 for p in spec.parents])
+                    keep.append(ev)
+                    d.parent_ev_slot = ctypes.cast(ev, ctypes.POINTER(ctypes.c_int32))
+                    pidx = torch.full((k, N), -1, dtype=torch.int32, device=device)
+                    for i, p in enumerate(spec.parents):
+                        if p in spec.free_samples:
+                            pidx[i] = domain_index(spec.free_samples[p], doms[i])
+                    keep.append(pidx)
+                    d.parent_sample_idx = pidx.data_ptr()
+            handle = ctypes.c_void_p()
+            torch.cuda.current_stream(device).synchronize()  # index arrays ready before the plan reads them
+            _native.check(lib.cbn_plan_create_direct(descs, len(plan.factors), N, ctypes.byref(handle)),
+                          "cbn_plan_create_direct")
+        plan.handle = handle
+        plan.keep = keep
+        plan.direct = True
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
 
     def _materialise_param(self, plan: Plan, device: torch.device):

@@ -12,8 +12,15 @@ kernels ``k_cpd_scatter`` / ``k_cpd_normalize`` (``cbn_bf_cpd_build``), and
 (``cbn_bf_cpd_eval``).  Values absent from the fitted domain give 0, exactly the
 reference's ``0 / (0 + 1e-10)``.
 
-The dense table is compiled lazily on first device use, so the host logic can
-be exercised without a GPU; every evaluation requires the HIP library.
+When the dense table would exceed ``dense_limit`` cells (continuous or
+high-cardinality columns: the table is prod(cards) while the reference only
+stores the U unique rows), ``fit`` compiles a SPARSE CPD instead: the U
+conditionals keyed by their mixed-radix domain index in an open-addressing
+hash table of 2^ceil(log2 2U) slots (``cbn_hash_build``), evaluated by
+``cbn_cpd_ref_eval`` and by direct inference plans (csrc/cbn_direct.hip).
+
+The table is compiled lazily on first device use, so the host logic can be
+exercised without a GPU; every evaluation requires the HIP library.
 """
 from __future__ import annotations
 
@@ -25,7 +32,29 @@ import torch
 from .. import _native
 from ..base.parameter_learning import BaseParameterLearningEstimator
 
-MAX_DENSE_CELLS = 1 << 28  # 1 GiB of fp32 per CPD
+MAX_DENSE_CELLS = 1 << 24  # 64 MiB of fp32 per dense CPD; larger CPDs are hashed
+
+
+def sparse_conditionals(cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool) -> torch.Tensor:
+    """Value of each unique row of a hashed CPD (cell = mixed-radix domain
+    index, node column last): joint / (parent marginal + 1e-10), the sums of
+    brute_force.py:240-254 over the rows sharing the row's parent values; the
+    root case (:205-214) keeps the joint."""
+    if not conditional:
+        return probs.clone()
+    pcell = torch.div(cell, card_node, rounding_mode="floor")
+    _, inv = torch.unique(pcell, return_inverse=True)
+    pmarg = torch.zeros(int(inv.max()) + 1 if inv.numel() else 0, dtype=torch.float32, device=probs.device)
+    pmarg.index_add_(0, inv, probs)
+    return probs / (pmarg[inv] + 1e-10)
+
+
+def hash_capacity(n: int) -> int:
+    """Slots of the open-addressing table for n keys: power of two >= 2n (load <= 1/2)."""
+    cap = 2
+    while cap < 2 * n:
+        cap *= 2
+    return cap
 
 
 class BruteForce(BaseParameterLearningEstimator):
@@ -37,6 +66,13 @@ class BruteForce(BaseParameterLearningEstimator):
         self.node_marginal: Optional[torch.Tensor] = None  # [card_node]
         self._rows = None
         self._probs = None
+        # dense CPD above this many cells -> hashed unique rows (sparse)
+        self.dense_limit = int(kwargs.get("dense_limit", config.get("dense_limit", MAX_DENSE_CELLS)
+                                          if isinstance(config, dict) else MAX_DENSE_CELLS))
+        self.sparse = False
+        self.hash_keys: Optional[torch.Tensor] = None  # int64 [capacity], -1 empty
+        self.hash_vals: Optional[torch.Tensor] = None  # float32 [capacity]
+        self._compiled = False
         self._setup_model(config, **kwargs)
 
     def _setup_model(self, config: Dict = None, **kwargs):
@@ -65,49 +101,93 @@ class BruteForce(BaseParameterLearningEstimator):
         self.domains = [torch.unique(self._rows[:, c]).contiguous() for c in range(self._rows.shape[1])]
         self.cpd = None
         self.node_marginal = None
+        self.hash_keys = self.hash_vals = None
+        self.sparse = False
+        self._compiled = False
 
     @property
     def cards(self) -> List[int]:
         return [int(d.numel()) for d in self.domains]
 
+    def n_cells(self) -> int:
+        n = 1
+        for c in self.cards:
+            n *= c
+        return n
+
     def compiled(self):
-        """Dense CPD on the device (built once per fit by the HIP kernels)."""
+        """The device CPD, built once per fit by the HIP kernels: the dense
+        table (returned), or -- above ``dense_limit`` cells -- the hashed
+        unique rows (``self.sparse``; returns None)."""
         assert self.mle_tensor is not None, "MLE tensor not fitted yet. Call _fit() first."
-        if self.cpd is not None:
+        if self._compiled:
             return self.cpd
         dev = _native.require_gpu(self.mle_tensor.device)
         lib = _native.load()
         cards = self.cards
-        n_cells = 1
-        for c in cards:
-            n_cells *= c
-        if n_cells > MAX_DENSE_CELLS:
-            raise _native.NativeError(
-                f"BruteForce dense CPD would hold {n_cells} cells (> {MAX_DENSE_CELLS}); "
-                "this estimator targets discrete domains")
+        n_cells = self.n_cells()
         with torch.cuda.device(dev):
-            cell = torch.zeros(self._rows.shape[0], dtype=torch.int64, device=dev)
+            rows = self._rows.to(dev)
+            probs = self._probs.to(dev)
+            cell = torch.zeros(rows.shape[0], dtype=torch.int64, device=dev)
             stride = 1
             idx_last = None
             for c in range(len(cards) - 1, -1, -1):
-                idx = torch.searchsorted(self.domains[c], self._rows[:, c].contiguous())
+                idx = torch.searchsorted(self.domains[c].to(dev), rows[:, c].contiguous())
                 if c == len(cards) - 1:
                     idx_last = idx
                 cell += idx * stride
                 stride *= cards[c]
-            cell32 = cell.to(torch.int32).contiguous()
-            cpd = torch.empty(n_cells, dtype=torch.float32, device=dev)
-            n_pcells = n_cells // cards[-1]
-            _native.check(lib.cbn_bf_cpd_build(_native.ptr(cell32), _native.ptr(self._probs),
-                                               cell32.numel(), n_pcells, cards[-1],
-                                               1 if len(cards) > 1 else 0, _native.ptr(cpd),
-                                               _native.stream_ptr(dev)), "cbn_bf_cpd_build")
             # P(node value) over all rows: the query=None case of brute_force.py:205-214
             marg = torch.zeros(cards[-1], dtype=torch.float32, device=dev)
-            marg.index_add_(0, idx_last, self._probs)
-        self.cpd = cpd.view(*cards)
+            marg.index_add_(0, idx_last, probs)
+            if n_cells <= self.dense_limit:
+                cell32 = cell.to(torch.int32).contiguous()
+                cpd = torch.empty(n_cells, dtype=torch.float32, device=dev)
+                n_pcells = n_cells // cards[-1]
+                _native.check(lib.cbn_bf_cpd_build(_native.ptr(cell32), _native.ptr(probs),
+                                                   cell32.numel(), n_pcells, cards[-1],
+                                                   1 if len(cards) > 1 else 0, _native.ptr(cpd),
+                                                   _native.stream_ptr(dev)), "cbn_bf_cpd_build")
+                self.cpd = cpd.view(*cards)
+            else:
+                self._build_sparse(lib, dev, cell, probs, cards[-1], len(cards) > 1)
         self.node_marginal = marg
+        self._compiled = True
         return self.cpd
+
+    def _build_sparse(self, lib, dev, cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool):
+        """Hashed CPD: value of unique row u = joint_u / (sum of joint over the
+        rows sharing u's parent values + 1e-10) (brute_force.py:240-254), the
+        root case without the division (:205-214)."""
+        vals = sparse_conditionals(cell, probs, card_node, conditional)
+        n = cell.numel()
+        cap = hash_capacity(n)
+        keys = torch.empty(cap, dtype=torch.int64, device=dev)
+        tvals = torch.empty(cap, dtype=torch.float32, device=dev)
+        cell = cell.contiguous()
+        vals = vals.contiguous()
+        _native.check(lib.cbn_hash_build(_native.ptr(cell), _native.ptr(vals), n, _native.ptr(keys),
+                                          _native.ptr(tvals), cap, _native.stream_ptr(dev)), "cbn_hash_build")
+        self.sparse = True
+        self.cpd = None
+        self.hash_keys, self.hash_vals = keys, tvals
+
+    def cpd_ref(self):
+        """(cbn_cpd_ref, host arrays it points into) of the compiled CPD."""
+        self.compiled()
+        n = len(self.domains)
+        doms = (ctypes.c_void_p * n)(*[d.data_ptr() for d in self.domains])
+        cards = (ctypes.c_int32 * n)(*self.cards)
+        r = _native.CpdRef()
+        r.n_cols = n
+        r.domains = ctypes.cast(doms, ctypes.POINTER(ctypes.c_void_p))
+        r.cards = ctypes.cast(cards, ctypes.POINTER(ctypes.c_int32))
+        if self.sparse:
+            r.keys, r.vals, r.capacity = self.hash_keys.data_ptr(), self.hash_vals.data_ptr(), self.hash_keys.numel()
+        else:
+            r.dense = self.cpd.data_ptr()
+        return r, (doms, cards)
 
     # ------------------------------------------------------------- eval ----
     def eval_points(self, points: torch.Tensor, table: Optional[torch.Tensor] = None,
@@ -115,15 +195,20 @@ class BruteForce(BaseParameterLearningEstimator):
         """cpd at float points [n, n_cols] (columns = parents..., node)."""
         cpd = self.compiled() if table is None else table
         domains = self.domains if domains is None else domains
-        dev = cpd.device
+        dev = self.hash_keys.device if cpd is None else cpd.device
         lib = _native.load()
         pts = points.to(device=dev, dtype=torch.float32).contiguous()
         n_cols = len(domains)
         assert pts.dim() == 2 and pts.shape[1] == n_cols
         out = torch.empty(pts.shape[0], dtype=torch.float32, device=dev)
-        dom_ptrs = (ctypes.c_void_p * n_cols)(*[d.data_ptr() for d in domains])
-        card_arr = (ctypes.c_int32 * n_cols)(*[int(d.numel()) for d in domains])
         with torch.cuda.device(dev):
+            if table is None and (self.sparse or n_cols > _native.CBN_MAX_PARENTS + 1):
+                ref, _keep = self.cpd_ref()
+                _native.check(lib.cbn_cpd_ref_eval(ctypes.byref(ref), _native.ptr(pts), pts.shape[0],
+                                                   _native.ptr(out), _native.stream_ptr(dev)), "cbn_cpd_ref_eval")
+                return out
+            dom_ptrs = (ctypes.c_void_p * n_cols)(*[d.data_ptr() for d in domains])
+            card_arr = (ctypes.c_int32 * n_cols)(*[int(d.numel()) for d in domains])
             _native.check(lib.cbn_bf_cpd_eval(_native.ptr(cpd.contiguous()), n_cols, dom_ptrs, card_arr,
                                               _native.ptr(pts), pts.shape[0], _native.ptr(out),
                                               _native.stream_ptr(dev)), "cbn_bf_cpd_eval")

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define CBN_AMD_ABI_VERSION 2
+#define CBN_AMD_ABI_VERSION 3
 
 #define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
 #define CBN_MAX_EVIDENCE 256 /* distinct evidence columns per query batch        */
@@ -85,6 +85,66 @@ int cbn_bf_cpd_build(const int32_t* cell, const float* prob, int64_t n_rows,
 int cbn_bf_cpd_eval(const float* cpd, int32_t n_cols, const float* const* domains,
                     const int32_t* domain_card, const float* points, int64_t n_points,
                     float* out, void* stream);
+
+/* ---- CPDs beyond dense tables: sparse (hashed) BruteForce CPDs and nodes
+ * with more than CBN_MAX_PARENTS parents.
+ *
+ * The reference answers BruteForce.get_prob for ANY fitted data with two
+ * equality scans over the unique training rows (brute_force.py:228-247), so
+ * continuous / high-cardinality columns work there at O(points x rows) per
+ * call.  A dense table over the columns' domains would hold prod(cards)
+ * cells; past a size limit the estimator keeps instead a hash table keyed by
+ * the row's mixed-radix domain index (parents in sorted order, node last;
+ * prod(cards) < 2^62) whose value is the row's conditional probability
+ * joint / (parent marginal + 1e-10) -- rows absent from the table give 0,
+ * exactly the reference's 0 / (0 + 1e-10).  Keys of empty slots are -1;
+ * capacity is a power of two >= 2 x rows (linear probing). */
+#define CBN_MAX_DIRECT_PARENTS 32
+
+/* Insert n (key, value) pairs (keys unique, >= 0) into a hash table of
+ * `capacity` slots (power of two); the table is cleared first. */
+int cbn_hash_build(const int64_t* keys, const float* vals, int64_t n, int64_t* table_keys, float* table_vals,
+                   int64_t capacity, void* stream);
+
+/* A BruteForce CPD over n_cols columns (parents in sorted order, node last):
+ * dense array [cards...] or hash table.  Host struct; pointers are device
+ * pointers except `domains` / `cards` (host arrays of n_cols entries). */
+typedef struct cbn_cpd_ref {
+    int32_t n_cols;
+    const float* const* domains;  /* sorted domain values of each column            */
+    const int32_t* cards;         /* |domain| of each column                        */
+    const float* dense;           /* dense CPD (NULL: sparse)                       */
+    const int64_t* keys;          /* sparse: table keys (-1 empty)                  */
+    const float* vals;            /* sparse: conditional probabilities              */
+    int64_t capacity;             /* sparse: slots (power of two)                   */
+} cbn_cpd_ref;
+
+/* BruteForce._get_prob (brute_force.py:185-257) on a dense or hashed CPD:
+ * out[i] = P(points[i]) -- points [n_points, n_cols] float32. */
+int cbn_cpd_ref_eval(const cbn_cpd_ref* cpd, const float* points, int64_t n_points, float* out, void* stream);
+
+/* One factor of a DIRECT plan: evaluated per (query, sample column) straight
+ * from its CPD (no per-plan table: the tables of these factors would have
+ * prod(observed cards) rows), any number of parents up to
+ * CBN_MAX_DIRECT_PARENTS.  Same kinds and sample-index conventions as
+ * cbn_factor_desc.  Root (SCALAR): cpd is the node marginal (n_cols = 1). */
+typedef struct cbn_direct_factor {
+    int32_t kind;                     /* CBN_FACTOR_*                                   */
+    int32_t n_parents;                /* k <= CBN_MAX_DIRECT_PARENTS (sorted order)     */
+    const int32_t* parent_ev_slot;    /* host [k]: evidence column or -1 (free)         */
+    const int32_t* node_sample_idx;   /* device [N]: node sample -> domain idx or -1    */
+    const int32_t* parent_sample_idx; /* device [k*N]: free-parent sample idx or -1     */
+    cbn_cpd_ref cpd;                  /* columns: parents..., node                      */
+} cbn_direct_factor;
+
+/* A plan whose factors are evaluated directly (BayesianNetwork.infer,
+ * bayesian_network.py:208-305, for networks whose dense factor tables do not
+ * fit): cbn_plan_run computes every (query, column) product in the
+ * reference's factor order, then the global-max division (raw + scale; the
+ * CBN_RUN_RAW launch for the sharded path).  query_max / query_write /
+ * the single-launch path are not available (CBN_E_UNSUPPORTED). */
+int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, int32_t n_samples,
+                           cbn_plan** plan);
 
 /* Build a plan for one (target node, observed-column set, N_max) of
  * BayesianNetwork.infer (bayesian_network.py:208-305).  Copies the
@@ -165,6 +225,7 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status);
 #define CBN_PLAN_FUSED 16      /* single-launch (grid barrier) path available */
 #define CBN_PLAN_PARAMETRIC 32 /* parametric CPDs (cbn_param.hip) */
 #define CBN_PLAN_VPL2 64       /* 8 output columns per lane */
+#define CBN_PLAN_DIRECT 128    /* direct plan (cbn_plan_create_direct) */
 int32_t cbn_plan_flags(const cbn_plan* plan);
 
 /* Test hook: mark the plan as if a single-launch call had timed out in its

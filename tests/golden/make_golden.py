@@ -132,6 +132,22 @@ CASES = [
     # configs[4] shape at a size where the 25-factor product stays finite: 5 x 5 grid, d = 4
     dict(name="grid5_d4_config4", data=("grid", 20000, 24, 5, 4), target="X24",
          ev=[f"X{i}" for i in range(24)], Q=64, N=4, ev_seed=204),
+    # direct plans (csrc/cbn_direct.hip): > 8 parents, hashed CPDs of
+    # high-cardinality and continuous columns
+    dict(name="wide10_free2", data=("wide", 4000, 31, 10), target="Y",
+         ev=[f"P{i}" for i in range(8)], Q=40, N=2, ev_seed=301),
+    dict(name="wide12_all", data=("wide", 4000, 32, 12), target="Y",
+         ev=[f"P{i}" for i in range(12)], Q=40, N=3, ev_seed=302),
+    dict(name="hicard40_all", data=("hicard", 20000, 33), target="E",
+         ev=["R0", "R1", "R2", "R3"], Q=64, N=16, ev_seed=303, seed=5),
+    dict(name="hicard40_free1", data=("hicard", 20000, 34), target="E",
+         ev=["R0", "R2", "R3"], Q=24, N=4, ev_seed=304, seed=6, missing=0.1),
+    dict(name="cont4_all", data=("cont", 8000, 35), target="X3",
+         ev=["X0", "X1", "X2"], Q=48, N=16, ev_seed=305, seed=7),
+    dict(name="cont4_free1", data=("cont", 8000, 36), target="X3",
+         ev=["X0", "X1"], Q=24, N=6, ev_seed=306, seed=8),
+    dict(name="cont4_free_support", data=("cont_free", 20000, 37), target="X3",
+         ev=["X0", "X1"], Q=24, N=8, ev_seed=307, seed=9),
 ]
 
 
@@ -139,10 +155,20 @@ def make_data(spec):
     if spec[0] == "chain":
         vals = spec[5] if len(spec) > 5 else None
         return chain_data(spec[1], spec[2], spec[3], spec[4], vals)
-    if spec[0] in ("alarm", "grid", "chain_stay"):
+    if spec[0] in ("alarm", "grid", "chain_stay", "wide", "hicard", "cont", "cont_free"):
         sys.path.insert(0, os.path.dirname(HERE))
-        from helpers import alarm_like_data, grid_data
+        from helpers import (alarm_like_data, continuous_data, continuous_free_data, grid_data, hicard_data,
+                             wide_data)
         from helpers import chain_data as chain_stay
+
+        if spec[0] == "wide":
+            return wide_data(spec[1], spec[2], k=spec[3])
+        if spec[0] == "hicard":
+            return hicard_data(spec[1], spec[2])
+        if spec[0] == "cont":
+            return continuous_data(spec[1], spec[2])
+        if spec[0] == "cont_free":
+            return continuous_free_data(spec[1], spec[2])
 
         if spec[0] == "chain_stay":  # bench.py's generator: X_i = X_{i-1} w.p. stay, else uniform
             return chain_stay(spec[1], spec[2], spec[3], spec[4], stay=spec[5])

@@ -170,3 +170,52 @@ def grid_data(S, seed, side=10, d=64, keep=0.8, noise=2):
             k = rng.random(S) < keep
             X[:, i] = np.where(k, (base + rng.integers(-noise, noise + 1, S)) % d, rng.integers(0, d, S))
     return X.astype(np.float32), [f"X{i}" for i in range(n)], edges
+
+
+def wide_data(S, seed, k=10, d=2, dy=3):
+    """One node Y with k parents P0..P{k-1} (uniform over d levels):
+    Y = (sum of the parents + noise) mod dy.  k > 8 is beyond the table
+    path's parent limit (direct plans)."""
+    rng = np.random.default_rng(seed)
+    P = rng.integers(0, d, (S, k))
+    Y = (P.sum(1) + rng.choice(3, S, p=[0.7, 0.2, 0.1])) % dy
+    X = np.concatenate([P, Y[:, None]], 1).astype(np.float32)
+    cols = [f"P{i}" for i in range(k)] + ["Y"]
+    return X, cols, [(f"P{i}", "Y") for i in range(k)]
+
+
+def hicard_data(S, seed, d=40, k=4):
+    """k uniform roots over d levels and a child E = (sum + noise) mod d:
+    the child's dense CPD has d^(k+1) cells (40^5 ~ 1e8: hashed)."""
+    rng = np.random.default_rng(seed)
+    R = rng.integers(0, d, (S, k))
+    E = (R.sum(1) + rng.choice(3, S, p=[0.6, 0.3, 0.1])) % d
+    X = np.concatenate([R, E[:, None]], 1).astype(np.float32)
+    cols = [f"R{i}" for i in range(k)] + ["E"]
+    return X, cols, [(f"R{i}", "E") for i in range(k)]
+
+
+def continuous_data(S, seed, decimals=1):
+    """Continuous roots X0..X2 ~ N(0, 2^2) rounded to ``decimals`` and
+    X3 = round(X0 + X1 + X2 + N(0, 1)): ~100 distinct values per root, the
+    dense CPD of X3 ~ 1e6 x 25 cells (hashed)."""
+    rng = np.random.default_rng(seed)
+    R = np.round(rng.normal(0, 2, (S, 3)), decimals)
+    X3 = np.round(R.sum(1) + rng.normal(0, 1, S), 0)
+    X = np.concatenate([R, X3[:, None]], 1).astype(np.float32)
+    cols = ["X0", "X1", "X2", "X3"]
+    return X, cols, [("X0", "X3"), ("X1", "X3"), ("X2", "X3")]
+
+
+def continuous_free_data(S, seed):
+    """Two continuous roots X0, X1 ~ N(0, 2^2) rounded to 2 decimals (~1 500
+    distinct values each), a 5-level root X2 and X3 = (round(X0 + X1) + X2)
+    mod 8: X3's dense CPD would be ~1e8 cells (hashed); with X0, X1 observed
+    and X2 free (N >= 8) every evidence row drawn from the data has support."""
+    rng = np.random.default_rng(seed)
+    R = np.round(rng.normal(0, 2, (S, 2)), 2)
+    X2 = rng.integers(0, 5, S)
+    X3 = (np.round(R.sum(1)).astype(np.int64) + X2) % 8
+    X = np.concatenate([R, X2[:, None], X3[:, None]], 1).astype(np.float32)
+    cols = ["X0", "X1", "X2", "X3"]
+    return X, cols, [("X0", "X3"), ("X1", "X3"), ("X2", "X3")]

@@ -1,0 +1,181 @@
+"""Direct inference plans (csrc/cbn_direct.hip) and hashed BruteForce CPDs.
+
+The reference's BruteForce (cbn/parameter_learning/brute_force.py:185-257)
+answers any fitted data by scanning its unique rows, so networks with > 8
+parents per node, continuous columns and high-cardinality domains all infer.
+Here those plans evaluate every factor per (query, sample column) straight
+from the CPD -- dense, or a hash table of the unique rows when the dense one
+would exceed ``dense_limit`` cells.  Checked against the reference's own
+outputs (tests/golden/make_golden.py: wide*, hicard*, cont4*), and every
+other golden re-run with the direct plans forced and with every CPD forced
+into the hash table.  Tolerance: rtol 1e-5, atol 1e-7 (north star); NaN rows
+(all-zero products, 0/0 in the reference) must be NaN here too.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from continuousbayesiannetwork_amd import BayesianNetwork, BruteForce, _native
+from golden_io import golden_names, load_golden
+from helpers import continuous_free_data, hicard_data, make_bn, sample_evidence, wide_data
+from oracle.ref_infer import OracleBN, OracleBruteForce
+
+pytestmark = pytest.mark.gpu
+RTOL, ATOL = 1e-5, 1e-7
+DIRECT_GOLDENS = ["wide10_free2", "wide12_all", "hicard40_all", "hicard40_free1", "cont4_all", "cont4_free1",
+                  "cont4_free_support"]
+OK_GOLDENS = [n for n in golden_names() if not load_golden(n)["meta"]["error"]]
+
+
+def _t(ev, dev):
+    return {k: torch.tensor(v, device=dev) for k, v in ev.items()}
+
+
+def _run_golden(name, gpu, force_direct=False, dense_limit=None):
+    g = load_golden(name)
+    m = g["meta"]
+    bn = make_bn(BayesianNetwork, m["edges"], m["columns"], g["data"], device=gpu)
+    bn.engine.force_direct = force_direct
+    if dense_limit is not None:
+        for nd in bn.nodes_obj.values():
+            nd.estimator.dense_limit = dense_limit
+    ev = None if m["evidence_none"] else _t({k: g["evidence"][k] for k in m["evidence"]}, gpu)
+    random.seed(m["seed"])
+    pdf, dom = bn.infer(m["target"], ev, N_max=m["N_max"])
+    np.testing.assert_array_equal(dom.cpu().numpy(), g["domain"])
+    np.testing.assert_allclose(pdf.cpu().numpy(), g["pdf"], rtol=RTOL, atol=ATOL)
+    return bn, pdf
+
+
+def _plan_flags(bn):
+    lib = _native.load()
+    return [lib.cbn_plan_flags(p.handle) for p in bn.engine._plans.values()]
+
+
+@pytest.mark.parametrize("name", DIRECT_GOLDENS)
+def test_direct_goldens_route_to_direct_plans(name, gpu):
+    """> 8 parents and CPDs above the dense limit take direct plans by themselves."""
+    bn, _ = _run_golden(name, gpu)
+    flags = _plan_flags(bn)
+    if flags:  # deterministic plans are cached; oversampled ones are rebuilt per call
+        assert all(f & _native.CBN_PLAN_DIRECT for f in flags)
+    if name.startswith(("hicard", "cont")):
+        tgt = load_golden(name)["meta"]["target"]
+        assert bn.nodes_obj[tgt].estimator.sparse
+
+
+@pytest.mark.parametrize("name", OK_GOLDENS)
+def test_forced_direct_matches_reference(name, gpu):
+    _run_golden(name, gpu, force_direct=True)
+
+
+@pytest.mark.parametrize("name", OK_GOLDENS)
+def test_forced_hashed_cpds_match_reference(name, gpu):
+    """Every CPD in the hash table (dense_limit = 1): the sparse representation
+    on the whole golden set, free parents and off-domain evidence included."""
+    bn, _ = _run_golden(name, gpu, dense_limit=1)
+    assert all(nd.estimator.sparse for nd in bn.nodes_obj.values() if nd.estimator._compiled and
+               len(nd.estimator.domains) > 0 and nd.estimator.n_cells() > 1)
+
+
+@pytest.mark.parametrize("dense_limit", [None, 1])
+def test_bruteforce_get_prob_wide_and_hashed(dense_limit, gpu):
+    """BruteForce._get_prob (brute_force.py:185-257) with 11 columns (beyond
+    the dense evaluator) and with a hashed CPD, on- and off-domain points."""
+    rng = np.random.default_rng(3)
+    k = 10
+    pd_ = rng.integers(0, 2, (k, 6000)).astype(np.float32)
+    nd_ = ((pd_.sum(0) + rng.integers(0, 2, 6000)) % 3).astype(np.float32)
+    ob = OracleBruteForce()
+    ob.fit(nd_, pd_)
+    kw = {} if dense_limit is None else {"dense_limit": dense_limit}
+    bf = BruteForce({"estimator_name": "brute_force"}, device=gpu, **kw)
+    bf.fit(torch.tensor(nd_, device=gpu), torch.tensor(pd_, device=gpu))
+    pts = rng.integers(-1, 4, (200, 5)).astype(np.float32)
+    q = rng.integers(0, 2, (200, k, 1)).astype(np.float32)
+    q[::9, 3, 0] = -1  # off-domain parent value
+    ref = ob.get_prob(pts, q)
+    got = bf.get_prob(torch.tensor(pts, device=gpu), torch.tensor(q, device=gpu)).cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+    assert (got[ref == 0] == 0).all() and (ref > 0).mean() > 0.05
+    assert bf.sparse == (dense_limit == 1)
+
+
+def test_continuous_get_prob_hashed(gpu):
+    """Continuous columns (~1 500 distinct values each): the CPD is hashed by
+    size; conditionals at data rows and at perturbed (absent) values."""
+    data, cols, _ = continuous_free_data(20000, 5)
+    ob = OracleBruteForce()
+    ob.fit(data[:, 3], data[:, :3].T)
+    bf = BruteForce({"estimator_name": "brute_force"}, device=gpu)
+    bf.fit(torch.tensor(data[:, 3], device=gpu), torch.tensor(data[:, :3].T.copy(), device=gpu))
+    rng = np.random.default_rng(1)
+    rows = rng.integers(0, 20000, 300)
+    q = data[rows, :3][:, :, None].copy()
+    q[::7, 0, 0] += 0.005  # off-domain
+    pts = np.tile(np.arange(8, dtype=np.float32), (300, 1))
+    ref = ob.get_prob(pts, q)
+    got = bf.get_prob(torch.tensor(pts, device=gpu), torch.tensor(q, device=gpu)).cpu().numpy()
+    assert bf.sparse
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+    assert (ref > 0).any(1).mean() > 0.8
+
+
+def test_direct_raw_scale_and_stepper_equal_infer(gpu):
+    """The raw launch (+ scale) and the sharded stepper on a direct plan give
+    the infer result bit for bit."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper
+
+    data, cols, edges = hicard_data(20000, 33)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = _t(sample_evidence(data, cols, ["R0", "R1", "R2", "R3"], 5000, 4), gpu)
+    a, _ = bn.infer("E", ev, N_max=40)
+    assert all(f & _native.CBN_PLAN_DIRECT for f in _plan_flags(bn))
+    rows, _, words, scale = bn.engine.infer_raw("E", ev, 40)
+    scale(rows, words)
+    np.testing.assert_array_equal(rows.cpu().numpy(), a.cpu().numpy())
+    for gather in (False, True):
+        st = ShardedStepper(bn, "E", 40, exchange_every=2, force_exchange=True, gather=gather)
+        outs = [st.step(ev)[0] for _ in range(3)]
+        st.wait()
+        torch.cuda.synchronize()
+        for o in outs:
+            np.testing.assert_array_equal(o.cpu().numpy(), a.cpu().numpy())
+        st.close()
+
+
+def test_direct_full_batch_matches_oracle(gpu):
+    """65 536 queries on the continuous network (hashed CPD, one free parent,
+    N_max above its cardinality: the random padding is redrawn per call):
+    sampled rows and the GPU's argmax row against the oracle, normalised by
+    the oracle's value of that argmax row (the reference divides by the max
+    of the whole batch)."""
+    data, cols, edges = continuous_free_data(20000, 37)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    evn = sample_evidence(data, cols, ["X0", "X1"], 65536, 11, missing_frac=0.05)
+    random.seed(21)
+    pdf, _ = bn.infer("X3", _t(evn, gpu), N_max=8)
+    pdf = pdf.cpu().numpy()
+    assert bn.nodes_obj["X3"].estimator.sparse
+    assert pdf.max() == 1.0
+    r_star = int(np.argmax(pdf.max(1)))
+    pick = sorted(set(range(0, 65536, 8191)) | {r_star})
+    random.seed(21)
+    raw = OracleBN(edges, cols, data).infer_raw("X3", {k: v[pick] for k, v in evn.items()}, 8)[0]
+    ref = raw / raw[pick.index(r_star)].max()
+    np.testing.assert_allclose(pdf[pick], ref, rtol=RTOL, atol=ATOL)
+
+
+def test_wide_node_many_parents_oracle(gpu):
+    """A 16-parent node (wide_data), every parent observed, off-domain values."""
+    data, cols, edges = wide_data(6000, 8, k=16)
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = sample_evidence(data, cols, [f"P{i}" for i in range(16)], 300, 2, missing_frac=0.02)
+    ref, rdom = ora.infer("Y", ev, 3)
+    pdf, dom = bn.infer("Y", _t(ev, gpu), N_max=3)
+    np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
+    np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    assert all(f & _native.CBN_PLAN_DIRECT for f in _plan_flags(bn))

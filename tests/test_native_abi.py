@@ -26,13 +26,17 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     lib = _native.load()
-    assert lib.cbn_abi_version() == 2 == _native.ABI_VERSION
+    assert lib.cbn_abi_version() == 3 == _native.ABI_VERSION
     # cbn_factor_desc: 3 int32 + 2*8 int32 + 3 pointers + 8 pointers (with alignment padding)
     assert ctypes.sizeof(_native.FactorDesc) == 4 * 19 + 4 + 8 * 11
     # cbn_param_model: 8 int32 (family, n_layers, width[5], act) + pointer + 2 float
     assert ctypes.sizeof(_native.ParamModel) == 4 * 8 + 8 + 8
     # cbn_param_factor: kind + 8 slots (+4 pad) + 2 pointers + model
     assert ctypes.sizeof(_native.ParamFactor) == 4 * 9 + 4 + 16 + ctypes.sizeof(_native.ParamModel)
+    # cbn_cpd_ref: n_cols (+4 pad) + 5 pointers + int64
+    assert ctypes.sizeof(_native.CpdRef) == 8 + 5 * 8 + 8
+    # cbn_direct_factor: 2 int32 + 3 pointers + cpd
+    assert ctypes.sizeof(_native.DirectFactor) == 8 + 3 * 8 + ctypes.sizeof(_native.CpdRef)
 
 
 def test_argument_errors_are_reported_without_gpu():
@@ -77,3 +81,64 @@ def test_param_argument_errors_are_reported_without_gpu():
     assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == -1
     m.scale = 1.0
     assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == 0  # empty: no launch
+
+
+def test_direct_argument_errors_are_reported_without_gpu():
+    """cbn_plan_create_direct / cbn_hash_build / cbn_cpd_ref_eval validate
+    their arguments before touching the device."""
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.cbn_plan_create_direct(None, 0, 4, ctypes.byref(h)) == -1
+    f = (_native.DirectFactor * 1)()
+    f[0].kind = 9
+    assert lib.cbn_plan_create_direct(f, 1, 4, ctypes.byref(h)) == -1
+    assert b"bad kind" in lib.cbn_last_error()
+    f[0].kind, f[0].n_parents = 2, 33  # above CBN_MAX_DIRECT_PARENTS
+    assert lib.cbn_plan_create_direct(f, 1, 4, ctypes.byref(h)) == -3
+    f[0].n_parents = 1
+    f[0].node_sample_idx = 16
+    f[0].cpd.n_cols = 3  # parents + node = 2
+    assert lib.cbn_plan_create_direct(f, 1, 4, ctypes.byref(h)) == -1
+    assert b"columns" in lib.cbn_last_error()
+    # capacity not a power of two / below 2n
+    assert lib.cbn_hash_build(None, None, 0, 16, 16, 12, None) == -1
+    assert lib.cbn_hash_build(16, 16, 5, 16, 16, 8, None) == -1
+    doms = (ctypes.c_void_p * 2)(16, 16)
+    cards = (ctypes.c_int32 * 2)(3, 0)
+    r = _native.CpdRef()
+    r.n_cols, r.dense = 2, 16
+    r.domains = ctypes.cast(doms, ctypes.POINTER(ctypes.c_void_p))
+    r.cards = ctypes.cast(cards, ctypes.POINTER(ctypes.c_int32))
+    assert lib.cbn_cpd_ref_eval(ctypes.byref(r), None, 0, None, None) == -1  # card 0
+    cards[1] = 4
+    assert lib.cbn_cpd_ref_eval(ctypes.byref(r), None, 0, None, None) == 0  # empty: no launch
+    r.dense, r.keys, r.vals, r.capacity = None, 16, 16, 6  # hashed, capacity not a power of two
+    assert lib.cbn_cpd_ref_eval(ctypes.byref(r), None, 0, None, None) == -1
+
+
+def test_sparse_conditionals_match_oracle_rows():
+    """The hashed CPD's values (host logic, CPU tensors) equal the oracle's
+    BruteForce conditional at every unique training row."""
+    import numpy as np
+    import torch
+
+    from continuousbayesiannetwork_amd.parameter_learning.brute_force import hash_capacity, sparse_conditionals
+    from oracle.ref_infer import OracleBruteForce
+
+    rng = np.random.default_rng(0)
+    pd_ = np.round(rng.normal(0, 1, (2, 3000)), 1).astype(np.float32)
+    nd_ = (np.round(pd_.sum(0)) % 4).astype(np.float32)
+    ob = OracleBruteForce()
+    ob.fit(nd_, pd_)
+    rows, probs = ob.mle[:, :-1], ob.mle[:, -1]
+    doms = [np.unique(rows[:, c]) for c in range(3)]
+    cell = np.zeros(rows.shape[0], np.int64)
+    stride = 1
+    for c in (2, 1, 0):
+        cell += np.searchsorted(doms[c], rows[:, c]) * stride
+        stride *= len(doms[c])
+    vals = sparse_conditionals(torch.tensor(cell), torch.tensor(probs), len(doms[2]), True).numpy()
+    ref = ob.get_prob(rows[:, 2:3], rows[:, :2, None])[:, 0]
+    np.testing.assert_allclose(vals, ref, rtol=1e-6, atol=0)
+    assert len(np.unique(cell)) == len(cell)
+    assert hash_capacity(len(cell)) >= 2 * len(cell) and hash_capacity(1) == 2 and hash_capacity(5) == 16
