@@ -69,7 +69,8 @@ struct alignas(16) PRec {
     int in_slot[kMaxP];
     float inv_scale;  // fp32 1 / scale (Newton-refined division by the scale)
     int free_mask;    // bit i: model input i is a free parent (sampled per combo)
-    int pad[5];
+    int pw_off;       // one-hidden-layer models: image offset of the pair-packed weights (0: none)
+    int pad[4];
 };
 static_assert(sizeof(PRec) == 128, "PRec layout");
 constexpr int kRecFloats = sizeof(PRec) / 4;
@@ -126,10 +127,79 @@ __device__ __forceinline__ float exp_split(float x) {
     return fmaf(r, pl * kLn2, r);
 }
 
+// Two fp32 lanes per VALU op: gfx950's packed fp32 FMA / MUL / ADD
+// (v_pk_*_f32) run two independent columns / hidden units per instruction at
+// the rate of one -- the parametric kernel is VALU-issue bound.  The packed
+// ops are the same IEEE operations, so a pair gives the bits of two scalar
+// evaluations.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 f2s(float a) { return f2{a, a}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// exp_split on a pair (the two v_exp_f32 are scalar: transcendentals do not pack)
+__device__ __forceinline__ f2 exp_split2(f2 x) {
+    constexpr float kL = 1.44269502162933349609375f;
+    constexpr float kLlo = 1.925963033500e-8f;
+    constexpr float kLn2 = 0.693147180559945309f;
+    x.x = x.x < -104.f ? -104.f : x.x;
+    x.y = x.y < -104.f ? -104.f : x.y;
+    const f2 ph = x * f2s(kL);
+    const f2 pl = fma2(x, f2s(kLlo), fma2(x, f2s(kL), -ph));
+    const f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
+    return fma2(r, pl * f2s(kLn2), r);
+}
+
+// div_nr on a pair (same operations; the IEEE fallback per component)
+__device__ __forceinline__ f2 div_nr2(f2 n, f2 d, f2 r) {
+    const f2 q = n * r;
+    f2 res = fma2(fma2(-d, q, n), r, q);
+    if (!(d.x <= 0x1p126f)) res.x = n.x / d.x;
+    if (!(d.y <= 0x1p126f)) res.y = n.y / d.y;
+    return res;
+}
+__device__ __forceinline__ f2 div_nr2(f2 n, f2 d) {
+    return div_nr2(n, d, f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)});
+}
+
+// tanh (nn.Tanh) within ~2 ulp in ~16 VALU slots (libm tanhf: ~30): |x| <
+// 0.625: x + x^3 P(x^2), the odd minimax polynomial of the Cephes tanhf;
+// else 1 - 2 / (1 + e^(2|x|)) (e^(2|x|) = inf -> 1); sign restored.  Both
+// branches are evaluated (lanes of a wave diverge) and selected; NaN
+// propagates through the second.
+template <typename T>
+__device__ __forceinline__ T tanh_poly(T ax) {
+    const T z = ax * ax;
+    T p = fma(z, T(-5.70498872745e-3f), T(2.06390887954e-2f));
+    p = fma(p, z, T(-5.37397155531e-2f));
+    p = fma(p, z, T(1.33314422036e-1f));
+    p = fma(p, z, T(-3.33332819422e-1f));
+    return fma(p * z, ax, ax);
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float small = tanh_poly(ax);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.88539008177792681472f);  // 2 log2(e)
+    const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);
+    return copysignf(ax < 0.625f ? small : big, x);
+}
+__device__ __forceinline__ f2 tanh_fast2(f2 x) {
+    const f2 ax = f2{fabsf(x.x), fabsf(x.y)};
+    const f2 z = ax * ax;
+    f2 p = fma2(z, f2s(-5.70498872745e-3f), f2s(2.06390887954e-2f));
+    p = fma2(p, z, f2s(-5.37397155531e-2f));
+    p = fma2(p, z, f2s(1.33314422036e-1f));
+    p = fma2(p, z, f2s(-3.33332819422e-1f));
+    const f2 small = fma2(p * z, ax, ax);
+    const f2 t = ax * f2s(2.88539008177792681472f);
+    const f2 u = f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f2s(1.f);
+    const f2 big = fma2(f2s(-2.f), f2{__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)}, f2s(1.f));
+    return f2{copysignf(ax.x < 0.625f ? small.x : big.x, x.x), copysignf(ax.y < 0.625f ? small.y : big.y, x.y)};
+}
+
 // activation_map of neural_network.py:10-18 (torch CPU formulas)
 __device__ __forceinline__ float act1(int act, float x) {
     switch (act) {
-        case CBN_ACT_TANH: return tanhf(x);
+        case CBN_ACT_TANH: return tanh_fast(x);
         case CBN_ACT_RELU: return x > 0.f ? x : 0.f;
         case CBN_ACT_SIGMOID:  // exp(-x) clamped below FLT_MAX: 1 / (1 + 3.3e38) for x < -88.7 (torch: 0)
             return div_nr(1.f, 1.f + exp_split(-x > 88.7f ? 88.7f : -x));  // NaN stays NaN
@@ -146,7 +216,7 @@ __device__ __forceinline__ void activate(int act, int w, float (&h)[H]) {
         case CBN_ACT_TANH:
 #pragma unroll
             for (int o = 0; o < H; ++o)
-                if (o < w) h[o] = tanhf(h[o]);
+                if (o < w) h[o] = tanh_fast(h[o]);
             break;
         case CBN_ACT_RELU:
 #pragma unroll
@@ -164,6 +234,13 @@ __device__ __forceinline__ void activate(int act, int w, float (&h)[H]) {
     }
 }
 
+template <int ACT>
+__device__ __forceinline__ f2 act2(int act, f2 x) {
+    if (ACT == CBN_ACT_TANH) return tanh_fast2(x);
+    if (ACT == CBN_ACT_RELU) return f2{x.x > 0.f ? x.x : 0.f, x.y > 0.f ? x.y : 0.f};
+    return f2{act1(act, x.x), act1(act, x.y)};
+}
+
 // One hidden layer (the reference's default, neural_network.py:37): stream
 // over the hidden units -- mu = b2 + sum_o W2[o] act(W1[o] . z + b1[o]) in o
 // order (the output layer's fma chain) -- four units per step, so the
@@ -176,18 +253,20 @@ __device__ __forceinline__ float mlp1(const float* __restrict__ W, int n_in, int
     const float* W2 = B1 + H;
     float mu = 0.f;
     int o = 0;
-    for (; o + 4 <= H; o += 4) {
-        float s[4];
+    for (; o + 4 <= H; o += 4) {  // units (o, o+1) and (o+2, o+3) as packed pairs
+        f2 h[2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float a = 0.f;
+        for (int u = 0; u < 2; ++u) {
+            f2 a = f2s(0.f);
 #pragma unroll
             for (int i = 0; i < kMaxP; ++i)
-                if (i < n_in) a = fmaf(W[(o + u) * n_in + i], z[i], a);
-            s[u] = a + B1[o + u];
+                if (i < n_in) a = fma2(f2{W[(o + 2 * u) * n_in + i], W[(o + 2 * u + 1) * n_in + i]}, f2s(z[i]), a);
+            h[u] = act2<ACT>(act, a + f2{B1[o + 2 * u], B1[o + 2 * u + 1]});
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) mu = fmaf(W2[o + u], act1(act, s[u]), mu);
+        mu = fmaf(W2[o], h[0].x, mu);
+        mu = fmaf(W2[o + 1], h[0].y, mu);
+        mu = fmaf(W2[o + 2], h[1].x, mu);
+        mu = fmaf(W2[o + 3], h[1].y, mu);
     }
     for (; o < H; ++o) {
         float a = 0.f;
@@ -197,6 +276,73 @@ __device__ __forceinline__ float mlp1(const float* __restrict__ W, int n_in, int
         mu = fmaf(W2[o], act1(act, a + B1[o]), mu);
     }
     return mu + W2[H];
+}
+
+// One hidden layer from the pair-packed weights (the query kernel's form of
+// mlp1; same operations in the same order): per unit pair P the record
+//   [W(2P, i), W(2P+1, i)] for i < NIN, [B1(2P), B1(2P+1)], [W2(2P), W2(2P+1)]
+// (2 NIN + 4 floats; a padding unit of odd H has zeros and is never summed),
+// then the output bias.  With NIN a compile-time constant every weight read
+// is an immediate-offset scalar load from one pointer, and each (unit pair,
+// input) weight pair sits in an SGPR pair the packed FMA takes as is.
+template <int ACT, int NIN>
+__device__ __forceinline__ float mlp1p(const float* __restrict__ PW, int H, const float (&z)[kMaxP], int act) {
+    constexpr int kRec = 2 * NIN + 4;
+    const int npairs = (H + 1) >> 1;
+    float mu = 0.f;
+    int P = 0;
+    for (; P + 2 <= npairs; P += 2, PW += 2 * kRec) {
+        f2 h[2], w2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const f2* R = reinterpret_cast<const f2*>(PW + u * kRec);
+            f2 a = f2s(0.f);
+#pragma unroll
+            for (int i = 0; i < NIN; ++i) a = fma2(R[i], f2s(z[i]), a);
+            h[u] = act2<ACT>(act, a + R[NIN]);
+            w2[u] = R[NIN + 1];
+        }
+        mu = fmaf(w2[0].x, h[0].x, mu);
+        mu = fmaf(w2[0].y, h[0].y, mu);
+        mu = fmaf(w2[1].x, h[1].x, mu);
+        mu = fmaf(w2[1].y, h[1].y, mu);
+    }
+    if (P < npairs) {
+        const f2* R = reinterpret_cast<const f2*>(PW);
+        f2 a = f2s(0.f);
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) a = fma2(R[i], f2s(z[i]), a);
+        const f2 h = act2<ACT>(act, a + R[NIN]);
+        const f2 w2 = R[NIN + 1];
+        mu = fmaf(w2.x, h.x, mu);
+        if (2 * P + 1 < H) mu = fmaf(w2.y, h.y, mu);
+        PW += kRec;
+    }
+    return mu + PW[0];
+}
+
+template <int ACT>
+__device__ __forceinline__ float mlp1p_nin(const float* __restrict__ PW, int n_in, int H, const float (&z)[kMaxP],
+                                           int act) {
+    switch (n_in) {  // wave-uniform
+        case 1: return mlp1p<ACT, 1>(PW, H, z, act);
+        case 2: return mlp1p<ACT, 2>(PW, H, z, act);
+        case 3: return mlp1p<ACT, 3>(PW, H, z, act);
+        case 4: return mlp1p<ACT, 4>(PW, H, z, act);
+        case 5: return mlp1p<ACT, 5>(PW, H, z, act);
+        case 6: return mlp1p<ACT, 6>(PW, H, z, act);
+        case 7: return mlp1p<ACT, 7>(PW, H, z, act);
+        default: return mlp1p<ACT, 8>(PW, H, z, act);
+    }
+}
+
+__device__ __forceinline__ float mlp1_packed(const PRec& r, const float* __restrict__ img, const float (&z)[kMaxP]) {
+    const float* PW = img + r.pw_off;
+    switch (r.m.act) {
+        case CBN_ACT_TANH: return mlp1p_nin<CBN_ACT_TANH>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_TANH);
+        case CBN_ACT_RELU: return mlp1p_nin<CBN_ACT_RELU>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_RELU);
+        default: return mlp1p_nin<0>(PW, r.m.width[0], r.m.width[1], z, r.m.act);
+    }
 }
 
 // mu = model(z): y = W x + b per nn.Linear (dot product first, then the bias:
@@ -301,21 +447,45 @@ __device__ __forceinline__ float pdf_eval(int mode, float scale, float inv_scale
     }
 }
 
+// pdf_t on two columns (packed; the same operations, so the same bits)
+template <int MODE>
+__device__ __forceinline__ f2 pdf2_t(float scale, float inv_scale, float norm, f2 x, float mu) {
+    if (MODE <= 1) {
+        const f2 t = MODE == 0 ? (x - f2s(mu)) : div_nr2(x - f2s(mu), f2s(scale), f2s(inv_scale));
+        return f2s(norm) * exp_split2(f2s(-0.5f) * (t * t));
+    }
+    const f2 d = MODE == 2 ? (x - f2s(mu)) : div_nr2(x - f2s(mu), f2s(scale), f2s(inv_scale));
+    const f2 e = exp_split2(-d);
+    const f2 u = f2s(1.f) + e;
+    return div_nr2(e, MODE == 2 ? u * u : f2s(scale) * (u * u));
+}
+
 // fx[j] += pdf(S[j]; mu) over the chunk (S, scale, norm wave-uniform; S rows
-// are padded to a multiple of kColPad, so no column predicates)
+// are padded to a multiple of kColPad, so no column predicates); column pairs packed
 template <int NC, int MODE>
 __device__ __forceinline__ void add_row_t(float (&fx)[NC], const float* __restrict__ S, float sc, float isc,
                                           float nm, float mu) {
+    static_assert(NC % 2 == 0, "column pairs");
 #pragma unroll
-    for (int j = 0; j < NC; ++j) fx[j] += pdf_t<MODE>(sc, isc, nm, S[j], mu);
+    for (int j = 0; j < NC; j += 2) {
+        const f2 p = pdf2_t<MODE>(sc, isc, nm, f2{S[j], S[j + 1]}, mu);
+        const f2 r = f2{fx[j], fx[j + 1]} + p;
+        fx[j] = r.x;
+        fx[j + 1] = r.y;
+    }
 }
 
 // acc[j] *= pdf(S[j]; mu): the M == 1 factor (a mean over size-1 axes is the pdf itself)
 template <int NC, int MODE>
 __device__ __forceinline__ void mul_row_t(float (&acc)[NC], const float* __restrict__ S, float sc, float isc,
                                           float nm, float mu) {
+    static_assert(NC % 2 == 0, "column pairs");
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * pdf_t<MODE>(sc, isc, nm, S[j], mu);
+    for (int j = 0; j < NC; j += 2) {
+        const f2 r = f2{acc[j], acc[j + 1]} * pdf2_t<MODE>(sc, isc, nm, f2{S[j], S[j + 1]}, mu);
+        acc[j] = r.x;
+        acc[j + 1] = r.y;
+    }
 }
 
 template <int NC, int MODE>
@@ -467,7 +637,9 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                             }
                         }
                     }
-                    add_row<NC, MODE>(mode, fx, S, sc, isc, nm, model_mu<HMAX, kQThreads>(r.m, W, z, deep));
+                    const float mu = (HMAX == 1 && r.pw_off) ? mlp1_packed(r, img, z)
+                                                             : model_mu<HMAX, kQThreads>(r.m, W, z, deep);
+                    add_row<NC, MODE>(mode, fx, S, sc, isc, nm, mu);
                 }
                 if (r.M > 1) {
                     const float Mf = (float)r.M;
@@ -635,6 +807,28 @@ int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const 
     for (int l = 0; l <= h.n_layers; ++l) m.width[l] = h.width[l];
     for (int l = 0; l < h.n_layers; ++l) n_weights += (long long)h.width[l + 1] * (h.width[l] + 1);
     return CBN_OK;
+}
+
+// [W1 (H x n_in), B1 (H), W2 (H), b2] (nn.Linear order, parametric.py
+// packed()) -> the pair records of mlp1p
+void pack_pairs(const std::vector<float>& w, int n_in, int H, std::vector<float>& pw) {
+    const int npairs = (H + 1) / 2;
+    const float* W1 = w.data();
+    const float* B1 = W1 + (size_t)H * n_in;
+    const float* W2 = B1 + H;
+    pw.assign((size_t)npairs * (2 * n_in + 4) + 1, 0.f);
+    float* o = pw.data();
+    for (int P = 0; P < npairs; ++P) {
+        for (int u = 0; u < 2; ++u) {
+            const int k = 2 * P + u;
+            if (k >= H) continue;
+            for (int i = 0; i < n_in; ++i) o[2 * i + u] = W1[(size_t)k * n_in + i];
+            o[2 * n_in + u] = B1[k];
+            o[2 * n_in + 2 + u] = W2[k];
+        }
+        o += 2 * n_in + 4;
+    }
+    *o = W2[H];
 }
 
 // LDS scratch of the deep-model path (>= 2 hidden layers): 2 x HMAX floats per thread
@@ -848,6 +1042,11 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         r.M = (int)M;
         r.w_off = (int)off;
         off += (nw + 3) & ~3LL;
+        if (r.m.n_layers == 2) {  // pair-packed copy for the query kernel (mlp1p)
+            const long long npairs = (r.m.width[1] + 1) / 2;
+            r.pw_off = (int)off;
+            off += (npairs * (2LL * r.m.width[0] + 4) + 1 + 3) & ~3LL;
+        }
         const long long row = (N + kColPad - 1) / kColPad * kColPad;  // padded: chunk reads never leave the row
         r.s_off = (int)off;
         off += row;
@@ -961,6 +1160,13 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         if (ok && r.fs_off)
             ok = hipMemcpy(pp->d_image + r.fs_off, h.input_samples, sizeof(float) * (size_t)r.m.width[0] * N,
                            hipMemcpyDeviceToDevice) == hipSuccess;
+        if (ok && r.pw_off) {
+            std::vector<float> w(nw), pw;
+            ok = hipMemcpy(w.data(), h.model.weights, sizeof(float) * nw, hipMemcpyDeviceToHost) == hipSuccess;
+            pack_pairs(w, r.m.width[0], r.m.width[1], pw);
+            ok = ok && hipMemcpy(pp->d_image + r.pw_off, pw.data(), sizeof(float) * pw.size(), hipMemcpyHostToDevice) ==
+                           hipSuccess;
+        }
     }
     ok = ok && hipDeviceSynchronize() == hipSuccess;
     if (ok && !consts.empty()) {
