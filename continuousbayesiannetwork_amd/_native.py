@@ -26,6 +26,8 @@ CBN_FACTOR_QUERY = 2
 
 CBN_MAX_LAYERS = 4
 CBN_MAX_WIDTH = 32
+CBN_MAX_MODEL_LAYERS = 64
+CBN_MAX_MODEL_WIDTH = 256
 CBN_FAMILY_GAUSS = 1
 CBN_FAMILY_LOGISTIC = 2
 CBN_ACT = {"tanh": 1, "relu": 2, "sigmoid": 3, "leakyrelu": 4, "gelu": 5, "elu": 6}
@@ -63,6 +65,7 @@ class ParamModel(ctypes.Structure):
         ("weights", ctypes.c_void_p),
         ("scale", ctypes.c_float),
         ("norm", ctypes.c_float),
+        ("widths", _c_int_p),
     ]
 
 
@@ -75,6 +78,7 @@ class ParamFactor(ctypes.Structure):
         ("input_samples", ctypes.c_void_p),
         ("node_samples", ctypes.c_void_p),
         ("model", ParamModel),
+        ("input_slots", _c_int_p),
     ]
 
 

@@ -113,17 +113,21 @@ __device__ __forceinline__ float div_nr(float n, float d) { return div_nr(n, d, 
 // low part of log2(e)), 2^hi by v_exp_f32, 2^lo ~ 1 + lo ln2 (|lo| <= 2^-24
 // |hi|).  x below -104 (exp underflows) is clamped so the residual stays
 // finite; NaN passes through (comparisons false).  v_exp_f32 returns 0 where
-// 2^hi is subnormal (hi < -126): such a density is < 1.2e-38 and flushes to
-// 0 (the reference keeps the subnormal) -- measured and bounded in
-// tests/test_gpu_param.py::test_density_accuracy_full_range.
+// 2^hi is subnormal (hi < -126), so there 2^(hi + 64) is scaled by 2^-64: the
+// subnormal results the reference keeps (a branch the wave skips unless a
+// lane needs it) -- bounded in tests/test_gpu_param.py::test_density_accuracy_full_range.
 __device__ __forceinline__ float exp_split(float x) {
+#pragma clang fp contract(off)
     constexpr float kL = 1.44269502162933349609375f;  // fp32(log2 e)
     constexpr float kLlo = 1.925963033500e-8f;       // log2 e - kL
     constexpr float kLn2 = 0.693147180559945309f;
     x = x < -104.f ? -104.f : x;
     const float ph = x * kL;
     const float pl = fmaf(x, kLlo, fmaf(x, kL, -ph));
-    const float r = __builtin_amdgcn_exp2f(ph);
+    float r = __builtin_amdgcn_exp2f(ph);
+    // ph + 64 is exact -- and must not be contracted into fma(x, kL, 64), whose
+    // different rounding pl would not correct
+    if (ph < -126.f) r = __builtin_amdgcn_exp2f(ph + 64.f) * 0x1p-64f;
     return fmaf(r, pl * kLn2, r);
 }
 
@@ -138,6 +142,7 @@ __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementw
 
 // exp_split on a pair (the two v_exp_f32 are scalar: transcendentals do not pack)
 __device__ __forceinline__ f2 exp_split2(f2 x) {
+#pragma clang fp contract(off)
     constexpr float kL = 1.44269502162933349609375f;
     constexpr float kLlo = 1.925963033500e-8f;
     constexpr float kLn2 = 0.693147180559945309f;
@@ -145,7 +150,11 @@ __device__ __forceinline__ f2 exp_split2(f2 x) {
     x.y = x.y < -104.f ? -104.f : x.y;
     const f2 ph = x * f2s(kL);
     const f2 pl = fma2(x, f2s(kLlo), fma2(x, f2s(kL), -ph));
-    const f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
+    f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
+    if (fminf(ph.x, ph.y) < -126.f) {  // subnormal results (see exp_split)
+        if (ph.x < -126.f) r.x = __builtin_amdgcn_exp2f(ph.x + 64.f) * 0x1p-64f;
+        if (ph.y < -126.f) r.y = __builtin_amdgcn_exp2f(ph.y + 64.f) * 0x1p-64f;
+    }
     return fma2(r, pl * f2s(kLn2), r);
 }
 
@@ -336,14 +345,40 @@ __device__ __forceinline__ float mlp1p_nin(const float* __restrict__ PW, int n_i
     }
 }
 
+// the other activations: one instantiation, input count at run time
+__device__ __forceinline__ float mlp1p_rt(const float* __restrict__ PW, int n_in, int H, const float (&z)[kMaxP],
+                                       int act) {
+    const int rec = 2 * n_in + 4;
+    const int npairs = (H + 1) >> 1;
+    float mu = 0.f;
+    for (int P = 0; P < npairs; ++P, PW += rec) {
+        const f2* R = reinterpret_cast<const f2*>(PW);
+        f2 a = f2s(0.f);
+#pragma unroll
+        for (int i = 0; i < kMaxP; ++i)
+            if (i < n_in) a = fma2(R[i], f2s(z[i]), a);
+        const f2 h = act2<0>(act, a + R[n_in]);
+        const f2 w2 = R[n_in + 1];
+        mu = fmaf(w2.x, h.x, mu);
+        if (2 * P + 1 < H) mu = fmaf(w2.y, h.y, mu);
+    }
+    return mu + PW[0];
+}
+
 __device__ __forceinline__ float mlp1_packed(const PRec& r, const float* __restrict__ img, const float (&z)[kMaxP]) {
     const float* PW = img + r.pw_off;
     switch (r.m.act) {
         case CBN_ACT_TANH: return mlp1p_nin<CBN_ACT_TANH>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_TANH);
         case CBN_ACT_RELU: return mlp1p_nin<CBN_ACT_RELU>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_RELU);
-        default: return mlp1p_nin<0>(PW, r.m.width[0], r.m.width[1], z, r.m.act);
+        default: return mlp1p_rt(PW, r.m.width[0], r.m.width[1], z, r.m.act);
     }
 }
+
+// mu of a query factor: HMAX 1 plans hold linear and one-hidden-layer models
+// (the latter always pair-packed)
+template <int HMAX>
+__device__ __forceinline__ float query_mu(const PRec& r, const float* __restrict__ img, const float* __restrict__ W,
+                                          const float (&z)[kMaxP], float* deep);
 
 // mu = model(z): y = W x + b per nn.Linear (dot product first, then the bias:
 // addmm's order), activation after every layer but the last.  HMAX = 0: the
@@ -417,6 +452,14 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
     }
 }
 
+template <int HMAX>
+__device__ __forceinline__ float query_mu(const PRec& r, const float* __restrict__ img, const float* __restrict__ W,
+                                          const float (&z)[kMaxP], float* deep) {
+    if (HMAX == 0) return model_mu<0>(r.m, W, z, deep);
+    if (HMAX == 1) return r.m.n_layers == 2 ? mlp1_packed(r, img, z) : model_mu<0>(r.m, W, z, deep);
+    return model_mu<HMAX, 512>(r.m, W, z, deep);
+}
+
 // Densities, in the reference's fp32 operation order (divisions within one
 // ulp, see div_nr; exp within ~2 ulp, see exp_split).  MODE: 0 Gauss with scale 1, 1 Gauss, 2 logistic with
 // scale 1, 3 logistic.  With scale == 1 exactly, (x - mu) / scale == x - mu.
@@ -460,18 +503,35 @@ __device__ __forceinline__ f2 pdf2_t(float scale, float inv_scale, float norm, f
     return div_nr2(e, MODE == 2 ? u * u : f2s(scale) * (u * u));
 }
 
-// fx[j] += pdf(S[j]; mu) over the chunk (S, scale, norm wave-uniform; S rows
-// are padded to a multiple of kColPad, so no column predicates); column pairs packed
+// s + x with the rounding error of the addition carried in c (TwoSum): the
+// sum over the M free-parent combos of a mean stays within ~1 ulp whatever M
+// (torch.mean's reduction is blocked/pairwise; a plain running fp32 sum over
+// N^k terms drifts by ~M/2 ulp)
+__device__ __forceinline__ void two_sum(float& s, float& c, float x) {
+    const float t = s + x;
+    const float z = t - s;
+    c += (s - (t - z)) + (x - z);
+    s = t;
+}
+
+// fx[j] (+ cx[j]) += pdf(S[j]; mu) over the chunk (S, scale, norm
+// wave-uniform; S rows are padded to a multiple of kColPad, so no column
+// predicates); column pairs packed
 template <int NC, int MODE>
-__device__ __forceinline__ void add_row_t(float (&fx)[NC], const float* __restrict__ S, float sc, float isc,
-                                          float nm, float mu) {
+__device__ __forceinline__ void add_row_t(float (&fx)[NC], float (&cx)[NC], const float* __restrict__ S, float sc,
+                                          float isc, float nm, float mu) {
     static_assert(NC % 2 == 0, "column pairs");
 #pragma unroll
     for (int j = 0; j < NC; j += 2) {
         const f2 p = pdf2_t<MODE>(sc, isc, nm, f2{S[j], S[j + 1]}, mu);
-        const f2 r = f2{fx[j], fx[j + 1]} + p;
-        fx[j] = r.x;
-        fx[j + 1] = r.y;
+        const f2 a = f2{fx[j], fx[j + 1]};
+        const f2 t = a + p;
+        const f2 z = t - a;
+        const f2 c = f2{cx[j], cx[j + 1]} + ((a - (t - z)) + (p - z));
+        fx[j] = t.x;
+        fx[j + 1] = t.y;
+        cx[j] = c.x;
+        cx[j + 1] = c.y;
     }
 }
 
@@ -489,16 +549,31 @@ __device__ __forceinline__ void mul_row_t(float (&acc)[NC], const float* __restr
 }
 
 template <int NC, int MODE>
-__device__ __forceinline__ void add_row(int mode, float (&fx)[NC], const float* __restrict__ S, float sc, float isc,
-                                        float nm, float mu) {
+__device__ __forceinline__ void add_row(int mode, float (&fx)[NC], float (&cx)[NC], const float* __restrict__ S,
+                                        float sc, float isc, float nm, float mu) {
     if (MODE < 4) {
-        add_row_t<NC, MODE < 4 ? MODE : 0>(fx, S, sc, isc, nm, mu);
+        add_row_t<NC, MODE < 4 ? MODE : 0>(fx, cx, S, sc, isc, nm, mu);
     } else {
         switch (mode) {
-            case 0: add_row_t<NC, 0>(fx, S, sc, isc, nm, mu); break;
-            case 1: add_row_t<NC, 1>(fx, S, sc, isc, nm, mu); break;
-            case 2: add_row_t<NC, 2>(fx, S, sc, isc, nm, mu); break;
-            default: add_row_t<NC, 3>(fx, S, sc, isc, nm, mu); break;
+            case 0: add_row_t<NC, 0>(fx, cx, S, sc, isc, nm, mu); break;
+            case 1: add_row_t<NC, 1>(fx, cx, S, sc, isc, nm, mu); break;
+            case 2: add_row_t<NC, 2>(fx, cx, S, sc, isc, nm, mu); break;
+            default: add_row_t<NC, 3>(fx, cx, S, sc, isc, nm, mu); break;
+        }
+    }
+}
+
+template <int NC, int MODE>
+__device__ __forceinline__ void mul_row(int mode, float (&acc)[NC], const float* __restrict__ S, float sc, float isc,
+                                        float nm, float mu) {
+    if (MODE < 4) {
+        mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, S, sc, isc, nm, mu);
+    } else {
+        switch (mode) {
+            case 0: mul_row_t<NC, 0>(acc, S, sc, isc, nm, mu); break;
+            case 1: mul_row_t<NC, 1>(acc, S, sc, isc, nm, mu); break;
+            case 2: mul_row_t<NC, 2>(acc, S, sc, isc, nm, mu); break;
+            default: mul_row_t<NC, 3>(acc, S, sc, isc, nm, mu); break;
         }
     }
 }
@@ -613,20 +688,15 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 const float* S = img + r.s_off + col0;
                 const int mode = mode_of(r.family, r.unit != 0);
                 const float sc = r.scale, isc = r.inv_scale, nm = r.norm;
-                if (HMAX == 0 && MODE < 4 && r.M == 1) {  // linear model, every parent observed
-                    mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, S, sc, isc, nm, model_mu<0>(r.m, W, z, deep));
+                if (r.M == 1) {  // every parent observed: x = pdf (a mean over size-1 axes)
+                    mul_row<NC, MODE>(mode, acc, S, sc, isc, nm, query_mu<HMAX>(r, img, W, z, deep));
+                } else {
+                    float fx[NC], cx[NC];
 #pragma unroll
-                    for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
-                    continue;
-                }
-                float fx[NC];
-#pragma unroll
-                for (int j = 0; j < NC; ++j) fx[j] = 0.f;
-                const float* FS = img + r.fs_off;
-                // M == 1 (every parent observed): one pass, x = pdf (a mean over size-1 axes)
-                const int fm = r.free_mask;
-                for (int c = 0; c < r.M; ++c) {
-                    if (fm) {
+                    for (int j = 0; j < NC; ++j) fx[j] = cx[j] = 0.f;
+                    const float* FS = img + r.fs_off;
+                    const int fm = r.free_mask;
+                    for (int c = 0; c < r.M; ++c) {
                         int cc = c;  // meshgrid 'ij' order: last free input fastest (node.py:335-375)
 #pragma unroll
                         for (int i = kMaxP - 1; i >= 0; --i) {
@@ -636,18 +706,12 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                                 cc = qd;
                             }
                         }
+                        add_row<NC, MODE>(mode, fx, cx, S, sc, isc, nm, query_mu<HMAX>(r, img, W, z, deep));
                     }
-                    const float mu = (HMAX == 1 && r.pw_off) ? mlp1_packed(r, img, z)
-                                                             : model_mu<HMAX, kQThreads>(r.m, W, z, deep);
-                    add_row<NC, MODE>(mode, fx, S, sc, isc, nm, mu);
-                }
-                if (r.M > 1) {
                     const float Mf = (float)r.M;
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) fx[j] = fx[j] / Mf;  // torch.mean = sum / count
+                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * ((fx[j] + cx[j]) / Mf);  // torch.mean = sum / count
                 }
-#pragma unroll
-                for (int j = 0; j < NC; ++j) acc[j] = acc[j] * fx[j];
             }
 #pragma unroll
             for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
@@ -717,7 +781,7 @@ k_param_const(float* __restrict__ img, const int* __restrict__ which, int N) {
     for (int j0 = 0; j0 < N; j0 += blockDim.x) {  // uniform trip count (model uses LDS scratch)
         const int j = j0 + threadIdx.x;
         const int js = j < N ? j : N - 1;
-        float s = 0.f;
+        float s = 0.f, sc = 0.f;
         float z[kMaxP];
 #pragma unroll
         for (int i = 0; i < kMaxP; ++i) z[i] = (i < n_in && r.in_slot[i] == CBN_INPUT_ONE) ? 1.f : 0.f;
@@ -731,8 +795,10 @@ k_param_const(float* __restrict__ img, const int* __restrict__ which, int N) {
                     cc = qd;
                 }
             }
-            s += pdf_eval(mode_of(r.family, unit), r.scale, r.inv_scale, r.norm, S[js], model_mu<HMAX>(r.m, W, z, deep));
+            two_sum(s, sc, pdf_eval(mode_of(r.family, unit), r.scale, r.inv_scale, r.norm, S[js],
+                                    model_mu<HMAX>(r.m, W, z, deep)));
         }
+        s = s + sc;
         if (j < N) C[j] = r.kind == CBN_FACTOR_SCALAR ? s : s / (float)r.M;
     }
     if (r.kind == CBN_FACTOR_SCALAR) {  // mean over the N sample points (dim 1 of [1, N])
@@ -775,6 +841,218 @@ k_param_eval(MDesc m, int family, int unit, float scale, float norm, const float
     }
 }
 
+// ------------------------------------------------------------------------
+// Generic kernels: models of any shape within CBN_MAX_MODEL_* (more than
+// kMaxP inputs, hidden layers wider than CBN_MAX_WIDTH or more than kMaxL
+// layers).  Thread per (query, 16-column chunk); the layer activations of a
+// thread live in two LDS buffers of `wbuf` floats (element k of a thread at
+// k * T + tid: consecutive lanes, consecutive banks), the weights stream
+// through wave-uniform scalar loads.  Same operations in the same order as
+// model_mu: per layer and unit the dot product over the inputs, then the
+// bias, then the activation (all but the last layer).
+struct alignas(16) GRec {
+    int kind, family, unit, M;
+    int n_layers, n_in, act, w_off;
+    int s_off, fs_off, c_off, widths_off;
+    int slots_off;
+    float scale, inv_scale, norm;
+};
+static_assert(sizeof(GRec) == 64, "GRec layout");
+constexpr int kGenNC = 16;
+
+__device__ float mlp_gen(const float* __restrict__ W, const int* __restrict__ widths, int n_layers, int act, float* A,
+                         float* B, int T) {
+    int win = widths[0];
+    float* src = A;
+    float* dst = B;
+    for (int l = 0; l < n_layers; ++l) {
+        const int wout = widths[l + 1];
+        const float* Bl = W + (long long)wout * win;
+        if (l == n_layers - 1) {  // output layer: one unit
+            float s = 0.f;
+            for (int i = 0; i < win; ++i) s = fmaf(W[i], src[i * T], s);
+            return s + Bl[0];
+        }
+        for (int o = 0; o < wout; ++o) {
+            const float* Wo = W + (long long)o * win;
+            float s = 0.f;
+            for (int i = 0; i < win; ++i) s = fmaf(Wo[i], src[i * T], s);
+            dst[o * T] = act1(act, s + Bl[o]);
+        }
+        W = Bl + wout;
+        float* t = src;
+        src = dst;
+        dst = t;
+        win = wout;
+    }
+    return 0.f;
+}
+
+// model inputs of combo c into A: evidence of query q, free-parent sample
+// points (meshgrid 'ij' order: the last free input fastest), constant 1
+__device__ __forceinline__ void gen_inputs(const float* __restrict__ img, const GRec& r, const PEv* ev, long long q,
+                                           int c, int N, float* A, int T) {
+    const int* slots = reinterpret_cast<const int*>(img + r.slots_off);
+    const float* FS = img + r.fs_off;
+    int cc = c;
+    for (int i = r.n_in - 1; i >= 0; --i) {
+        const int sl = slots[i];
+        float v = 1.f;  // CBN_INPUT_ONE
+        if (sl >= 0) {
+            v = gload(ev->p[sl], q);
+        } else if (sl == CBN_INPUT_FREE) {
+            const int qd = cc / N;
+            v = FS[i * N + (cc - qd * N)];
+            cc = qd;
+        }
+        A[i * T] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_param_query_gen(const float* __restrict__ img, int nf, PEv ev, long long Q,
+                                                         int N, int L, int wbuf, int n_words,
+                                                         unsigned* __restrict__ max_out, float* __restrict__ out) {
+    extern __shared__ float smem_g[];
+    const int T = blockDim.x;
+    float* A = smem_g + threadIdx.x;
+    float* B = A + wbuf * T;
+    const GRec* rec = reinterpret_cast<const GRec*>(img);
+    unsigned lmaxb = 0;
+    const long long tasks = Q * L;
+    for (long long t = blockIdx.x * (long long)T + threadIdx.x; t < tasks; t += (long long)gridDim.x * T) {
+        const int l = (int)(t / Q);
+        const long long q = t - (long long)l * Q;
+        const int col0 = l * kGenNC;
+        const int ncol = min(kGenNC, N - col0);
+        float acc[kGenNC];
+#pragma unroll
+        for (int j = 0; j < kGenNC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        for (int f = 0; f < nf; ++f) {
+            const GRec& r = rec[f];
+            if (r.kind != CBN_FACTOR_QUERY) {
+                const float* c = img + r.c_off + col0;
+#pragma unroll
+                for (int j = 0; j < kGenNC; ++j) acc[j] = acc[j] * c[j];
+                continue;
+            }
+            const float* S = img + r.s_off + col0;
+            const float* W = img + r.w_off;
+            const int* widths = reinterpret_cast<const int*>(img + r.widths_off);
+            const int mode = mode_of(r.family, r.unit != 0);
+            if (r.M == 1) {
+                gen_inputs(img, r, &ev, q, 0, N, A, T);
+                const float mu = mlp_gen(W, widths, r.n_layers, r.act, A, B, T);
+#pragma unroll
+                for (int j = 0; j < kGenNC; ++j) acc[j] = acc[j] * pdf_eval(mode, r.scale, r.inv_scale, r.norm, S[j], mu);
+                continue;
+            }
+            float fx[kGenNC], cx[kGenNC];
+#pragma unroll
+            for (int j = 0; j < kGenNC; ++j) fx[j] = cx[j] = 0.f;
+            for (int c = 0; c < r.M; ++c) {
+                gen_inputs(img, r, &ev, q, c, N, A, T);
+                const float mu = mlp_gen(W, widths, r.n_layers, r.act, A, B, T);
+#pragma unroll
+                for (int j = 0; j < kGenNC; ++j) two_sum(fx[j], cx[j], pdf_eval(mode, r.scale, r.inv_scale, r.norm, S[j], mu));
+            }
+            const float Mf = (float)r.M;
+#pragma unroll
+            for (int j = 0; j < kGenNC; ++j) acc[j] = acc[j] * ((fx[j] + cx[j]) / Mf);  // torch.mean = sum / count
+        }
+        float* o = out + q * N + col0;
+#pragma unroll
+        for (int j = 0; j < kGenNC; ++j)
+            if (j < ncol) {
+                o[j] = acc[j];
+                lmaxb = max(lmaxb, __float_as_uint(acc[j]));  // NaN bits outrank every non-negative float
+            }
+    }
+    __shared__ unsigned wm[256 / kWave];
+    const unsigned wmx = wave_max_u(lmaxb);
+    if ((threadIdx.x & (kWave - 1)) == 0) wm[threadIdx.x / kWave] = wmx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned m = 0;
+        for (int i = 0; i < T / kWave; ++i) m = max(m, wm[i]);
+        max_out[blockIdx.x] = m;
+    }
+    if (blockIdx.x == 0)
+        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += T) max_out[i] = 0u;
+}
+
+// query-independent factors of a generic plan (k_param_const's semantics)
+__global__ void __launch_bounds__(256) k_param_const_gen(float* __restrict__ img, const int* __restrict__ which, int N,
+                                                         int wbuf) {
+    extern __shared__ float smem_g[];
+    const int T = blockDim.x;
+    float* A = smem_g + threadIdx.x;
+    float* B = A + wbuf * T;
+    const GRec& r = reinterpret_cast<const GRec*>(img)[which[blockIdx.x]];
+    const float* S = img + r.s_off;
+    float* C = img + r.c_off;
+    const int* widths = reinterpret_cast<const int*>(img + r.widths_off);
+    const int mode = mode_of(r.family, r.unit != 0);
+    for (int j0 = 0; j0 < N; j0 += T) {
+        const int j = j0 + threadIdx.x;
+        const int js = j < N ? j : N - 1;
+        float s = 0.f, sc = 0.f;
+        for (int c = 0; c < r.M; ++c) {
+            gen_inputs(img, r, nullptr, 0, c, N, A, T);
+            two_sum(s, sc, pdf_eval(mode, r.scale, r.inv_scale, r.norm, S[js],
+                                    mlp_gen(img + r.w_off, widths, r.n_layers, r.act, A, B, T)));
+        }
+        s = s + sc;
+        if (j < N) C[j] = r.kind == CBN_FACTOR_SCALAR ? s : s / (float)r.M;
+    }
+    if (r.kind == CBN_FACTOR_SCALAR) {  // mean over the N sample points (dim 1 of [1, N])
+        __syncthreads();
+        __shared__ float xs;
+        if (threadIdx.x == 0) {
+            float t = 0.f;
+            for (int j = 0; j < N; ++j) t += C[j];
+            xs = t / (float)N;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < N; j += blockDim.x) C[j] = xs;
+    }
+}
+
+struct GWidths {
+    int w[CBN_MAX_MODEL_LAYERS + 1];
+};
+
+// Estimator get_prob for a generic model: thread per row
+__global__ void __launch_bounds__(256) k_param_eval_gen(GWidths gw, int n_layers, int act, int family, int unit,
+                                                        float scale, float norm, const float* __restrict__ W,
+                                                        const float* __restrict__ pts, long long n_rows, int n_pts,
+                                                        const float* __restrict__ query, int wbuf,
+                                                        float* __restrict__ out) {
+    extern __shared__ float smem_g[];
+    __shared__ int widths[CBN_MAX_MODEL_LAYERS + 1];
+    for (int l = threadIdx.x; l <= n_layers; l += blockDim.x) widths[l] = gw.w[l];
+    __syncthreads();
+    const int T = blockDim.x;
+    float* A = smem_g + threadIdx.x;
+    float* B = A + wbuf * T;
+    const int n_in = widths[0];
+    const int mode = mode_of(family, unit != 0);
+    const float inv_scale = 1.f / scale;
+    for (long long r = blockIdx.x * (long long)T + threadIdx.x; r < n_rows; r += (long long)gridDim.x * T) {
+        for (int i = 0; i < n_in; ++i) A[i * T] = query ? query[r * n_in + i] : 1.f;
+        const float mu = mlp_gen(W, widths, n_layers, act, A, B, T);
+        for (int v = 0; v < n_pts; ++v)
+            out[r * n_pts + v] = pdf_eval(mode, scale, inv_scale, norm, pts[r * n_pts + v], mu);
+    }
+}
+
+// threads per block of the generic kernels: the two per-thread LDS buffers
+// of wbuf floats must fit the dynamic LDS
+int gen_threads(int wbuf) {
+    for (int T = 256; T >= 64; T >>= 1)
+        if ((size_t)2 * wbuf * T * sizeof(float) <= (size_t)(kLdsBudget - 512)) return T;
+    return 0;
+}
+
 // model kernel class: 0 linear, 1 one hidden layer (streamed), 32 deeper
 // (first hidden layer in registers, further ones in LDS)
 int hmax_for(const MDesc& m) {
@@ -785,27 +1063,61 @@ int hmax_for(const MDesc& m) {
     return 32;
 }
 
-int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const char* what, int idx) {
+// Model shape of a cbn_param_model (widths[] when given, else width[]),
+// validated against the generic kernel's limits.  `fast`: the shape the
+// register-resident kernels take (<= kMaxP inputs and either one hidden layer
+// of any width -- streamed -- or <= kMaxL layers of <= CBN_MAX_WIDTH units).
+struct HostModel {
+    int n_layers = 0;
+    int act = 0;
+    std::vector<int> w;
+    bool fast = false;
+    long long n_weights = 0;
+    int wmax = 0;  // widest input / hidden layer
+};
+
+int resolve_model(const cbn_param_model& h, HostModel& m, const char* what, int idx) {
     if (h.family != CBN_FAMILY_GAUSS && h.family != CBN_FAMILY_LOGISTIC)
         return set_err(CBN_E_ARG, "%s %d: bad family %d", what, idx, h.family);
-    if (h.n_layers < 1 || h.n_layers > kMaxL)
-        return set_err(CBN_E_LIMIT, "%s %d: %d layers (1..%d)", what, idx, h.n_layers, kMaxL);
-    if (h.width[0] < 1 || h.width[0] > kMaxP)
-        return set_err(CBN_E_LIMIT, "%s %d: %d model inputs (1..%d)", what, idx, h.width[0], kMaxP);
-    if (h.width[h.n_layers] != 1) return set_err(CBN_E_ARG, "%s %d: the last layer must have 1 output", what, idx);
-    for (int l = 1; l < h.n_layers; ++l)
-        if (h.width[l] < 1 || h.width[l] > CBN_MAX_WIDTH)
-            return set_err(CBN_E_LIMIT, "%s %d: hidden width %d (1..%d)", what, idx, h.width[l], CBN_MAX_WIDTH);
+    if (h.n_layers < 1 || h.n_layers > CBN_MAX_MODEL_LAYERS)
+        return set_err(CBN_E_LIMIT, "%s %d: %d layers (1..%d)", what, idx, h.n_layers, CBN_MAX_MODEL_LAYERS);
+    if (h.n_layers > kMaxL && !h.widths)
+        return set_err(CBN_E_ARG, "%s %d: %d layers need the widths array", what, idx, h.n_layers);
+    m.n_layers = h.n_layers;
+    m.act = h.act;
+    m.w.assign(h.n_layers + 1, 0);
+    for (int l = 0; l <= h.n_layers; ++l) m.w[l] = h.widths ? h.widths[l] : h.width[l];
+    if (m.w[0] < 1 || m.w[0] > CBN_MAX_MODEL_WIDTH)
+        return set_err(CBN_E_LIMIT, "%s %d: %d model inputs (1..%d)", what, idx, m.w[0], CBN_MAX_MODEL_WIDTH);
+    if (m.w[h.n_layers] != 1) return set_err(CBN_E_ARG, "%s %d: the last layer must have 1 output", what, idx);
+    int hid = 0;
+    for (int l = 1; l < h.n_layers; ++l) {
+        if (m.w[l] < 1 || m.w[l] > CBN_MAX_MODEL_WIDTH)
+            return set_err(CBN_E_LIMIT, "%s %d: hidden width %d (1..%d)", what, idx, m.w[l], CBN_MAX_MODEL_WIDTH);
+        hid = std::max(hid, m.w[l]);
+    }
     if (h.n_layers > 1 && (h.act < CBN_ACT_TANH || h.act > CBN_ACT_ELU))
         return set_err(CBN_E_ARG, "%s %d: bad activation %d", what, idx, h.act);
     if (!h.weights) return set_err(CBN_E_ARG, "%s %d: null weights", what, idx);
     if (!(h.scale > 0.f)) return set_err(CBN_E_ARG, "%s %d: scale must be > 0", what, idx);
+    m.n_weights = 0;
+    for (int l = 0; l < h.n_layers; ++l) m.n_weights += (long long)m.w[l + 1] * (m.w[l] + 1);
+    m.wmax = std::max(m.w[0], hid);
+    m.fast = h.n_layers <= kMaxL && m.w[0] <= kMaxP && (h.n_layers <= 2 || hid <= CBN_MAX_WIDTH);
+    return CBN_OK;
+}
+
+// the register-resident kernels' descriptor of a fast model
+int check_model(const cbn_param_model& h, MDesc& m, long long& n_weights, const char* what, int idx) {
+    HostModel hm;
+    const int rc = resolve_model(h, hm, what, idx);
+    if (rc) return rc;
+    if (!hm.fast) return set_err(CBN_E_LIMIT, "%s %d: model shape needs the generic kernel", what, idx);
     memset(&m, 0, sizeof(m));
-    m.n_layers = h.n_layers;
-    m.act = h.act;
-    n_weights = 0;
-    for (int l = 0; l <= h.n_layers; ++l) m.width[l] = h.width[l];
-    for (int l = 0; l < h.n_layers; ++l) n_weights += (long long)h.width[l + 1] * (h.width[l] + 1);
+    m.n_layers = hm.n_layers;
+    m.act = hm.act;
+    for (int l = 0; l <= hm.n_layers; ++l) m.width[l] = hm.w[l];
+    n_weights = hm.n_weights;
     return CBN_OK;
 }
 
@@ -874,6 +1186,9 @@ struct ParamPlan {
     float* d_image = nullptr;
     int* d_which = nullptr;
     int image_floats = 0;
+    bool generic = false;  // GRec image, k_param_query_gen (models beyond the fast kernels)
+    int wbuf = 0;          // generic: floats per LDS activation buffer
+    int gT = 0;            // generic: threads per block
 };
 }  // namespace cbn
 
@@ -942,6 +1257,22 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     } else {
         for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
     }
+    if (pp->generic) {
+        for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
+        const int L = (pp->N + kGenNC - 1) / kGenNC;
+        const long long tasks = n_queries * L;
+        long long grid = std::max(1LL, std::min((tasks + pp->gT - 1) / pp->gT, (long long)pp->max_slots));
+        const size_t lds = (size_t)2 * pp->wbuf * pp->gT * sizeof(float);
+        allow_deep(&k_param_query_gen);
+        const bool raw = (flags & CBN_RUN_RAW) != 0;
+        unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
+        hipLaunchKernelGGL(k_param_query_gen, dim3((unsigned)grid), dim3(pp->gT), lds, s, pp->d_image, pp->nf, ev,
+                           (long long)n_queries, pp->N, L, pp->wbuf, pp->max_slots, words, out);
+        PHIP_TRY(hipGetLastError());
+        if (raw) return CBN_OK;
+        if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_plan_run: out must be 16-B aligned");
+        return launch_scale(out, n_queries * (long long)pp->N, words, pp->max_slots, max_bits, s);
+    }
     const long long QW = (n_queries + kWave - 1) / kWave;
     // column chunk: linear models (mu costs a few FMAs) take 8 columns per lane
     // (<= 64 VGPRs: 8 waves per SIMD); MLPs keep whole rows up to 32 columns
@@ -987,6 +1318,139 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     return launch_scale(out, n_queries * (long long)pp->N, words, pp->max_slots, max_bits, s);
 }
 
+namespace {
+// Plan of a network with a model beyond the fast kernels: GRec image
+// (records, then per factor widths / input slots as ints, weights, node
+// samples, free-input samples, query-independent row)
+int create_param_generic(const cbn_param_factor* factors, int n_factors, int N, cbn_plan** plan) {
+    std::vector<GRec> recs(n_factors);
+    std::vector<HostModel> hm(n_factors);
+    std::vector<int> consts;
+    long long off = (long long)n_factors * (sizeof(GRec) / 4);
+    const long long row = (N + kColPad - 1) / kColPad * kColPad;
+    int ns = 0, wbuf = 1;
+    for (int f = 0; f < n_factors; ++f) {
+        const cbn_param_factor& h = factors[f];
+        GRec& r = recs[f];
+        memset(&r, 0, sizeof(r));
+        int rc = resolve_model(h.model, hm[f], "factor", f);
+        if (rc) return rc;
+        const HostModel& m = hm[f];
+        if (h.kind < CBN_FACTOR_SCALAR || h.kind > CBN_FACTOR_QUERY)
+            return set_err(CBN_E_ARG, "factor %d: bad kind %d", f, h.kind);
+        if (!h.node_samples) return set_err(CBN_E_ARG, "factor %d: null node samples", f);
+        if (m.w[0] > kMaxP && !h.input_slots)
+            return set_err(CBN_E_ARG, "factor %d: %d inputs need the input_slots array", f, m.w[0]);
+        int n_obs = 0, n_free = 0;
+        long long M = 1;
+        for (int i = 0; i < m.w[0]; ++i) {
+            const int sl = h.input_slots ? h.input_slots[i] : h.input_slot[i];
+            if (sl >= 0) {
+                if (sl >= CBN_MAX_EVIDENCE) return set_err(CBN_E_LIMIT, "factor %d: evidence slot %d", f, sl);
+                ns = std::max(ns, sl + 1);
+                ++n_obs;
+            } else if (sl == CBN_INPUT_FREE) {
+                ++n_free;
+                M *= N;
+                if (M >= (1LL << 31)) return set_err(CBN_E_LIMIT, "factor %d: too many free-parent combos", f);
+            } else if (sl != CBN_INPUT_ONE) {
+                return set_err(CBN_E_ARG, "factor %d: bad input slot %d", f, sl);
+            }
+        }
+        if (n_free > 0 && !h.input_samples) return set_err(CBN_E_ARG, "factor %d: free inputs without samples", f);
+        if ((h.kind == CBN_FACTOR_QUERY) != (n_obs > 0))
+            return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
+        if (h.kind == CBN_FACTOR_SCALAR && n_free > 0) return set_err(CBN_E_ARG, "factor %d: SCALAR with free inputs", f);
+        r.kind = h.kind;
+        r.family = h.model.family;
+        r.unit = h.model.scale == 1.f ? 1 : 0;
+        r.M = (int)M;
+        r.n_layers = m.n_layers;
+        r.n_in = m.w[0];
+        r.act = m.act;
+        r.scale = h.model.scale;
+        r.inv_scale = 1.f / h.model.scale;
+        r.norm = h.model.norm;
+        r.widths_off = (int)off;
+        off += (m.n_layers + 1 + 3) & ~3LL;
+        r.slots_off = (int)off;
+        off += (m.w[0] + 3) & ~3LL;
+        r.w_off = (int)off;
+        off += (m.n_weights + 3) & ~3LL;
+        r.s_off = (int)off;
+        off += row;
+        if (n_free > 0) {
+            r.fs_off = (int)off;
+            off += ((long long)m.w[0] * N + 3) & ~3LL;
+        }
+        if (h.kind != CBN_FACTOR_QUERY) {
+            r.c_off = (int)off;
+            off += row;
+            consts.push_back(f);
+        }
+        if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "parametric plan image too large");
+        wbuf = std::max(wbuf, m.wmax);
+    }
+    const int T = gen_threads(wbuf);
+    if (T == 0) return set_err(CBN_E_LIMIT, "parametric plan: layers of %d units exceed the LDS", wbuf);
+    // host copy of the record / int region (weights and samples are copied device to device)
+    std::vector<float> host((size_t)off, 0.f);
+    memcpy(host.data(), recs.data(), sizeof(GRec) * n_factors);
+    for (int f = 0; f < n_factors; ++f) {
+        const cbn_param_factor& h = factors[f];
+        int* wi = reinterpret_cast<int*>(host.data() + recs[f].widths_off);
+        for (int l = 0; l <= hm[f].n_layers; ++l) wi[l] = hm[f].w[l];
+        int* si = reinterpret_cast<int*>(host.data() + recs[f].slots_off);
+        for (int i = 0; i < hm[f].w[0]; ++i) si[i] = h.input_slots ? h.input_slots[i] : h.input_slot[i];
+    }
+    ParamPlan* pp = new ParamPlan();
+    pp->generic = true;
+    pp->nf = n_factors;
+    pp->N = N;
+    pp->ns = ns;
+    pp->wbuf = wbuf;
+    pp->gT = T;
+    pp->image_floats = (int)off;
+    pp->max_slots = std::min(4 * num_cu(), kMaxSlots);
+    cbn_plan* P = new cbn_plan();
+    P->param = pp;
+    P->nf = n_factors;
+    P->ns = ns;
+    P->N = N;
+    bool ok = hipMalloc(&pp->d_image, sizeof(float) * (size_t)off) == hipSuccess &&
+              hipMalloc(&pp->d_which, sizeof(int) * std::max<size_t>(consts.size(), 1)) == hipSuccess &&
+              hipMalloc(&P->d_sync, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    ok = ok && hipMemcpy(pp->d_image, host.data(), sizeof(float) * (size_t)off, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
+    ok = ok && (consts.empty() ||
+                hipMemcpy(pp->d_which, consts.data(), sizeof(int) * consts.size(), hipMemcpyHostToDevice) == hipSuccess);
+    for (int f = 0; ok && f < n_factors; ++f) {
+        const cbn_param_factor& h = factors[f];
+        const GRec& r = recs[f];
+        ok = hipMemcpy(pp->d_image + r.w_off, h.model.weights, sizeof(float) * hm[f].n_weights,
+                       hipMemcpyDeviceToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(pp->d_image + r.s_off, h.node_samples, sizeof(float) * N, hipMemcpyDeviceToDevice) ==
+                       hipSuccess;
+        if (ok && r.fs_off)
+            ok = hipMemcpy(pp->d_image + r.fs_off, h.input_samples, sizeof(float) * (size_t)r.n_in * N,
+                           hipMemcpyDeviceToDevice) == hipSuccess;
+    }
+    ok = ok && hipDeviceSynchronize() == hipSuccess;
+    if (ok && !consts.empty()) {
+        allow_deep(&k_param_const_gen);
+        hipLaunchKernelGGL(k_param_const_gen, dim3((unsigned)consts.size()), dim3(T),
+                           (size_t)2 * wbuf * T * sizeof(float), nullptr, pp->d_image, pp->d_which, N, wbuf);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    }
+    if (!ok) {
+        cbn_plan_destroy(P);
+        return set_err(CBN_E_HIP, "cbn_plan_create_param: device allocation/upload/build failed");
+    }
+    *plan = P;
+    return CBN_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, int32_t n_samples, cbn_plan** plan) {
@@ -994,6 +1458,12 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         return set_err(CBN_E_ARG, "cbn_plan_create_param: bad arguments");
     *plan = nullptr;
     const int N = n_samples;
+    for (int f = 0; f < n_factors; ++f) {  // any model beyond the fast kernels: the whole plan runs generic
+        HostModel hm;
+        const int rc = resolve_model(factors[f].model, hm, "factor", f);
+        if (rc) return rc;
+        if (!hm.fast || getenv("CBN_PARAM_GENERIC")) return create_param_generic(factors, n_factors, N, plan);
+    }
     std::vector<PRec> recs(n_factors);
     std::vector<int> consts;
     const long long cst_off = (long long)n_factors * kRecFloats;  // {0, 1}: constant model inputs
@@ -1014,7 +1484,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         long long M = 1;
         for (int i = 0; i < kMaxP; ++i) r.in_slot[i] = kInputNone;
         for (int i = 0; i < r.m.width[0]; ++i) {
-            const int sl = h.input_slot[i];
+            const int sl = h.input_slots ? h.input_slots[i] : h.input_slot[i];
             if (sl >= 0) {
                 if (sl >= CBN_MAX_EVIDENCE) return set_err(CBN_E_LIMIT, "factor %d: evidence slot %d", f, sl);
                 ns = std::max(ns, sl + 1);
@@ -1189,13 +1659,31 @@ int cbn_param_eval(const cbn_param_model* model, const float* points, int64_t n_
                    const float* query, int32_t root_bias_only, float* out, void* stream) {
     if (!model || n_rows < 0 || n_points < 0 || (n_rows > 0 && n_points > 0 && (!points || !out)))
         return set_err(CBN_E_ARG, "cbn_param_eval: bad arguments");
+    HostModel hm;
+    int rc = resolve_model(*model, hm, "model", 0);
+    if (rc) return rc;
+    if (root_bias_only && hm.n_layers != 1) return set_err(CBN_E_ARG, "cbn_param_eval: bias-only needs a linear model");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!hm.fast || getenv("CBN_PARAM_GENERIC")) {
+        const int T = gen_threads(hm.wmax);
+        if (T == 0) return set_err(CBN_E_LIMIT, "cbn_param_eval: layers of %d units exceed the LDS", hm.wmax);
+        if (n_rows == 0 || n_points == 0) return CBN_OK;
+        GWidths gw;
+        memset(&gw, 0, sizeof(gw));
+        for (int l = 0; l <= hm.n_layers; ++l) gw.w[l] = hm.w[l];
+        const long long blocks = std::max(1LL, std::min<long long>((n_rows + T - 1) / T, 8192));
+        allow_deep(&k_param_eval_gen);
+        hipLaunchKernelGGL(k_param_eval_gen, dim3((unsigned)blocks), dim3(T), (size_t)2 * hm.wmax * T * sizeof(float),
+                           s, gw, hm.n_layers, hm.act, model->family, model->scale == 1.f ? 1 : 0, model->scale,
+                           model->norm, model->weights, points, (long long)n_rows, (int)n_points, query, hm.wmax, out);
+        PHIP_TRY(hipGetLastError());
+        return CBN_OK;
+    }
     MDesc m;
     long long nw = 0;
-    int rc = check_model(*model, m, nw, "model", 0);
+    rc = check_model(*model, m, nw, "model", 0);
     if (rc) return rc;
-    if (root_bias_only && m.n_layers != 1) return set_err(CBN_E_ARG, "cbn_param_eval: bias-only needs a linear model");
     if (n_rows == 0 || n_points == 0) return CBN_OK;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const long long blocks = std::max(1LL, std::min<long long>((n_rows + kThreads - 1) / kThreads, 8192));
     const int unit = model->scale == 1.f ? 1 : 0;
 #define CBN_EVAL(H)                                                                                                 \

@@ -317,28 +317,31 @@ class InferenceEngine:
                 est = self.bn.nodes_obj[spec.node].estimator
                 root = not spec.parents
                 model, w = est.model_desc(root=root, device=device)
-                keep.append(w)
+                keep += [w, getattr(model, "_widths_keep", None)]
                 d = descs[f]
                 d.kind = spec.kind
                 d.model = model
-                k = int(model.width[0])
-                if root:
-                    for i in range(k):
-                        d.input_slot[i] = _native.CBN_INPUT_ONE
-                else:
+                k = int(model.widths[0]) if model.widths else int(model.width[0])
+                slots = [_native.CBN_INPUT_ONE] * k
+                if not root:
                     if len(spec.parents) != k:
                         raise _native.NativeError(f"node {spec.node}: model has {k} inputs, {len(spec.parents)} parents")
-                    if k > CBN_MAX_PARENTS:
-                        raise _native.NativeError(f"node {spec.node}: {k} parents > {CBN_MAX_PARENTS}")
                     samples = torch.zeros((k, N), dtype=torch.float32, device=device)
                     for i, p in enumerate(spec.parents):
                         if p in spec.observed:
-                            d.input_slot[i] = slot_of[p]
+                            slots[i] = slot_of[p]
                         else:
-                            d.input_slot[i] = _native.CBN_INPUT_FREE
+                            slots[i] = _native.CBN_INPUT_FREE
                             samples[i] = spec.free_samples[p].to(device=device, dtype=torch.float32)
                     keep.append(samples)
                     d.input_samples = samples.data_ptr()
+                if k <= CBN_MAX_PARENTS:
+                    for i, v in enumerate(slots):
+                        d.input_slot[i] = v
+                else:  # more inputs than the fixed array: the input_slots array
+                    arr = (ctypes.c_int32 * k)(*slots)
+                    keep.append(arr)
+                    d.input_slots = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
                 ns = spec.node_samples.to(device=device, dtype=torch.float32).contiguous()
                 keep.append(ns)
                 d.node_samples = ns.data_ptr()

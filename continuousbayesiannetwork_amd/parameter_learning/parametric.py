@@ -114,18 +114,23 @@ class _Parametric(BaseParameterLearningEstimator):
         here as the linear model [0, b] on the constant input 1; the logistic
         models run on the constant input 1 (neural_network.py:111-114)."""
         w, widths, act, scale, norm = self.packed(device)
-        if len(widths) - 1 > _native.CBN_MAX_LAYERS or max(widths[1:-1] or [1]) > _native.CBN_MAX_WIDTH:
+        if len(widths) - 1 > _native.CBN_MAX_MODEL_LAYERS or max(widths) > _native.CBN_MAX_MODEL_WIDTH:
             raise _native.NativeError(
-                f"model shape {widths} beyond the kernel limits ({_native.CBN_MAX_LAYERS} layers, "
-                f"{_native.CBN_MAX_WIDTH} units per hidden layer)")
+                f"model shape {widths} beyond the kernel limits ({_native.CBN_MAX_MODEL_LAYERS} layers, "
+                f"{_native.CBN_MAX_MODEL_WIDTH} units per layer)")
         if root and self.bias_only_root:
             w = torch.stack([torch.zeros((), dtype=torch.float32, device=w.device), w[widths[0]]]).contiguous()
             widths = [1, 1]
         m = _native.ParamModel()
         m.family = self.family
         m.n_layers = len(widths) - 1
-        for i, v in enumerate(widths):
-            m.width[i] = v
+        if m.n_layers <= _native.CBN_MAX_LAYERS:
+            for i, v in enumerate(widths):
+                m.width[i] = v
+        else:  # deeper models: the widths array (kept alive with the struct)
+            arr = (ctypes.c_int32 * len(widths))(*widths)
+            m.widths = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
+            m._widths_keep = arr
         m.act = act
         m.weights = w.data_ptr()
         m.scale = scale

@@ -247,8 +247,13 @@ int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* 
  *              d = (x - mu) / s;  pdf = exp(-d) / (s * (1 + exp(-d))^2)
  * mu = an nn.Linear stack: y = W x + b per layer, the activation after every
  * layer but the last (neural_network.py:45-54); one layer = a linear model. */
-#define CBN_MAX_LAYERS 4     /* nn.Linear layers per model          */
-#define CBN_MAX_WIDTH 32     /* units per hidden layer (reference defaults: 16, 32) */
+#define CBN_MAX_LAYERS 4     /* layers of the fixed-size width[] form (deeper: widths) */
+#define CBN_MAX_WIDTH 32     /* hidden units of the register-resident fast kernels: models
+                                with one hidden layer of any width and <= CBN_MAX_PARENTS
+                                inputs, or <= 4 layers of <= 32 units; larger models run
+                                the generic kernel (activations in LDS)                 */
+#define CBN_MAX_MODEL_LAYERS 64   /* generic kernel: nn.Linear layers                    */
+#define CBN_MAX_MODEL_WIDTH 256   /* generic kernel: inputs / units of any layer         */
 #define CBN_FAMILY_GAUSS 1
 #define CBN_FAMILY_LOGISTIC 2
 #define CBN_ACT_TANH 1       /* activation_map of neural_network.py:10-18 */
@@ -262,12 +267,14 @@ int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* 
 
 typedef struct cbn_param_model {
     int32_t family;                     /* CBN_FAMILY_*                                  */
-    int32_t n_layers;                   /* 1..CBN_MAX_LAYERS                             */
+    int32_t n_layers;                   /* 1..CBN_MAX_MODEL_LAYERS                       */
     int32_t width[CBN_MAX_LAYERS + 1];  /* width[0] = inputs, width[n_layers] = 1         */
     int32_t act;                        /* CBN_ACT_* (ignored when n_layers == 1)         */
     const float* weights;               /* device: per layer W[out][in] row-major, then b[out] */
     float scale;                        /* sigma = exp(log_sigma) / s = exp(log_scale), fp32 */
     float norm;                         /* GAUSS: 1 / (sigma * sqrt(2 pi)) as fp32 ops; else 0 */
+    const int32_t* widths;              /* host [n_layers + 1] or NULL: replaces width[]
+                                           (required when n_layers > CBN_MAX_LAYERS)      */
 } cbn_param_model;
 
 /* One ancestor's factor of BayesianNetwork.infer for a parametric estimator.
@@ -284,6 +291,8 @@ typedef struct cbn_param_factor {
     const float* input_samples;           /* device [width[0]][N]: rows of FREE inputs */
     const float* node_samples;            /* device [N]: the node's evaluation points  */
     cbn_param_model model;
+    const int32_t* input_slots;           /* host [width[0]] or NULL: replaces input_slot[]
+                                             (required for > CBN_MAX_PARENTS inputs)   */
 } cbn_param_factor;
 
 /* Plan of one (target, observed set, N_max) over parametric factors, run by

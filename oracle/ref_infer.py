@@ -158,7 +158,10 @@ class OracleParametric:
             mu = (np.zeros((x.shape[0], 1), np.float32) + self.layers[-1][1]).astype(np.float32)
         else:
             mu = self.mu(np.ones((x.shape[0], 1), np.float32))
-        s = np.exp(self.log_scale).astype(np.float32)
+        # the reference's scale is torch.exp of the fp32 log-scale parameter
+        # (linear_regression.py:91, neural_network.py:120); numpy's float32 exp
+        # can differ by an ulp, which (x - mu) / s amplifies by t^2 in the density
+        s = np.float32(torch.exp(torch.tensor(self.log_scale, dtype=torch.float32)).item())
         if self.family == "gauss":
             norm = (np.float32(1) / (s * np.sqrt(np.float32(2 * np.pi)))).astype(np.float32)
             t = ((x - mu) / s).astype(np.float32)
@@ -338,7 +341,11 @@ class OracleBN:
                 dims = tuple(range(1, pdf.ndim - 1))
             else:
                 dims = (1,)
-            x = pdf.astype(np.float32).mean(axis=dims, dtype=np.float32)
+            # torch.mean's CPU reduction is cascaded (error ~ a few ulp for any
+            # count); numpy's float32 mean over several axes accumulates
+            # sequentially (error ~ count x ulp: 1e-3 at 4^10 combos), so the
+            # mean is accumulated in float64 and rounded once
+            x = pdf.astype(np.float32).mean(axis=dims, dtype=np.float64).astype(np.float32)
             out = (out * x).astype(np.float32)
         if out.size == 0:
             raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")

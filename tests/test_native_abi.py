@@ -29,10 +29,10 @@ def test_abi_version_and_struct_layout():
     assert lib.cbn_abi_version() == 3 == _native.ABI_VERSION
     # cbn_factor_desc: 3 int32 + 2*8 int32 + 3 pointers + 8 pointers (with alignment padding)
     assert ctypes.sizeof(_native.FactorDesc) == 4 * 19 + 4 + 8 * 11
-    # cbn_param_model: 8 int32 (family, n_layers, width[5], act) + pointer + 2 float
-    assert ctypes.sizeof(_native.ParamModel) == 4 * 8 + 8 + 8
-    # cbn_param_factor: kind + 8 slots (+4 pad) + 2 pointers + model
-    assert ctypes.sizeof(_native.ParamFactor) == 4 * 9 + 4 + 16 + ctypes.sizeof(_native.ParamModel)
+    # cbn_param_model: 8 int32 (family, n_layers, width[5], act) + pointer + 2 float + widths pointer
+    assert ctypes.sizeof(_native.ParamModel) == 4 * 8 + 8 + 8 + 8
+    # cbn_param_factor: kind + 8 slots (+4 pad) + 2 pointers + model + input_slots pointer
+    assert ctypes.sizeof(_native.ParamFactor) == 4 * 9 + 4 + 16 + ctypes.sizeof(_native.ParamModel) + 8
     # cbn_cpd_ref: n_cols (+4 pad) + 5 pointers + int64
     assert ctypes.sizeof(_native.CpdRef) == 8 + 5 * 8 + 8
     # cbn_direct_factor: 2 int32 + 3 pointers + cpd
@@ -73,9 +73,16 @@ def test_param_argument_errors_are_reported_without_gpu():
     assert b"bad family" in lib.cbn_last_error()
     m = _native.ParamModel()
     m.family, m.n_layers = 1, 3
-    m.width[0], m.width[1], m.width[2], m.width[3] = 2, 64, 8, 1  # hidden width above CBN_MAX_WIDTH
+    m.width[0], m.width[1], m.width[2], m.width[3] = 2, 300, 8, 1  # hidden width above CBN_MAX_MODEL_WIDTH
     m.act, m.weights, m.scale = 1, 16, 1.0
     assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == -3
+    m.n_layers = 6  # deeper than width[] without the widths array
+    assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == -1
+    widths = (ctypes.c_int32 * 7)(2, 64, 64, 64, 64, 64, 1)
+    m.widths = ctypes.cast(widths, ctypes.POINTER(ctypes.c_int32))
+    assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == 0  # generic: empty, no launch
+    m.widths = None
+    m.n_layers = 3
     m.width[1] = 8
     m.scale = -1.0
     assert lib.cbn_param_eval(ctypes.byref(m), None, 0, 0, None, 0, None, None) == -1
