@@ -460,7 +460,9 @@ def test_ten_parent_parametric_node(observed, gpu):
 def test_subnormal_densities_in_infer(gpu):
     """Factors whose densities fall below 2^-126 inside a full infer (a sharp
     LinearRegression, sigma = 0.03): the unnormalised products agree with the
-    oracle's float32 ones to rtol 1e-5 plus two subnormal steps, and the
+    oracle's float32 ones to rtol 1e-5 plus eight subnormal steps (2^-146: a
+    subnormal density carries its few-ulp error as an absolute one, and the
+    product rounds it once more), and the
     normalised marginals to the north-star tolerance."""
     rng = np.random.default_rng(9)
     S = 3000
@@ -479,6 +481,6 @@ def test_subnormal_densities_in_infer(gpu):
     tiny = 2.0 ** -126
     sub = (ref_raw > 0) & (ref_raw < tiny)
     assert sub.sum() > 100  # the case is exercised
-    np.testing.assert_allclose(raw, ref_raw, rtol=RTOL, atol=2.0 ** -148)
+    np.testing.assert_allclose(raw, ref_raw, rtol=RTOL, atol=2.0 ** -146)
     scale(rows, words)
     np.testing.assert_allclose(rows.cpu().numpy(), ref_raw / ref_raw.max(), rtol=RTOL, atol=ATOL)
