@@ -1,7 +1,10 @@
 """Time the REFERENCE's own BayesianNetwork.infer on CPU for the bench workload
 (BASELINE configs[1]) on a bounded query sample.  Runs only where
 /root/reference exists (this container); the GPU box uses bench.py's oracle
-port instead.  Usage: python tools/time_reference_cpu.py [n_queries] [threads]"""
+port instead.  Usage: python tools/time_reference_cpu.py [n_queries] [threads] [processes]
+(processes > 1: the sample split into one chunk per process, each running the
+reference with one torch thread -- the layout of bench.py's parallel port;
+per-chunk normalisation does not change the work)."""
 import os
 import sys
 import time
@@ -16,9 +19,23 @@ from helpers import chain_data, sample_evidence  # noqa: E402
 from make_golden import _load_reference  # noqa: E402
 
 
+_BN = None
+
+
+def _chunk(ev):
+    import contextlib
+    import io
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        _BN.infer("X19", ev, N_max=32)
+    return True
+
+
 def main():
+    global _BN
     q = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     th = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    procs = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     torch.set_num_threads(th)
     import networkx as nx
     import pandas as pd
@@ -38,10 +55,22 @@ def main():
 
     with contextlib.redirect_stdout(io.StringIO()):
         bn.infer("X19", {k: v[:8] for k, v in ev.items()}, N_max=d)
-        t0 = time.perf_counter()
-        bn.infer("X19", ev, N_max=d)
-        t = time.perf_counter() - t0
-    print(f"reference BayesianNetwork.infer, chain20 d32, {q} queries, {th} torch threads: "
+        if procs > 1:
+            import multiprocessing as mp
+
+            _BN = bn
+            cuts = [q * i // procs for i in range(procs + 1)]
+            jobs = [{k: v[cuts[i]:cuts[i + 1]] for k, v in ev.items()} for i in range(procs)]
+            with mp.get_context("fork").Pool(procs) as pool:
+                pool.map(_chunk, [{k: v[:8] for k, v in ev.items()}] * procs, chunksize=1)
+                t0 = time.perf_counter()
+                pool.map(_chunk, jobs, chunksize=1)
+                t = time.perf_counter() - t0
+        else:
+            t0 = time.perf_counter()
+            bn.infer("X19", ev, N_max=d)
+            t = time.perf_counter() - t0
+    print(f"reference BayesianNetwork.infer, chain20 d32, {q} queries, {th} torch threads x {procs} processes: "
           f"{t:.3f} s -> {q / t:.1f} queries/s")
 
 
