@@ -4,7 +4,19 @@ nodes, target = the last node (every other node is an ancestor: a 100-factor
 product per query).  The reference's factors for a node whose parents are all
 observed are CPD rows (no marginalisation), so there is no dense d x d
 contraction on this path (no MFMA).  Batches of 65 536 and
-262 144 queries; writes gpurun_out/bench_grid.json."""
+262 144 queries; writes gpurun_out/bench_grid_keep*.json.
+
+Headline: the PEAKED network (keep 0.995, noise 0), whose 100-factor products
+stay finite.  keep 0.8 / noise 2 is DEGENERATE: every fp32 product underflows
+to 0 and every marginal is 0/0 = NaN (exactly what the reference returns),
+so its rate is reported but labelled.
+
+Roofline: each query gathers one 64-float row (256 B) of every factor table
+from the plan image (85 MB: beyond the 32 MiB of L2, inside the 256 MiB
+Infinity Cache); the gather rate is compared with the guide's gather
+figures: rows shared through an XCD's L2 16.8-18.8 TB/s, uniformly random
+rows of a 38 MB table (Infinity Cache) 8.6 TB/s (MI355X_MICROARCH.md
+'Indexed rows').  ``--profile``: one workload, 10 calls (for rocprofv3)."""
 import json
 import os
 import sys
@@ -20,11 +32,13 @@ from helpers import grid_data, make_bn, sample_evidence  # noqa: E402
 
 
 def main():
-    for keep, noise in ((0.8, 2), (0.995, 0)):
-        run(keep, noise)
+    prof = "--profile" in sys.argv
+    cases = ((0.995, 0),) if prof else ((0.995, 0), (0.8, 2))
+    for keep, noise in cases:
+        run(keep, noise, prof)
 
 
-def run(keep, noise):
+def run(keep, noise, prof=False):
     """keep=0.8, noise=2: every fp32 product of the 100 factors underflows (NaN
     rows, as in the reference); keep=0.995, noise=0: peaked CPDs whose products
     stay finite -- same plan shape, same work per query."""
@@ -37,7 +51,7 @@ def run(keep, noise):
     fit_s = time.time() - t0
     out = {"workload": f"grid 10x10, {len(edges)} edges, d={d}, N_max={d}, evidence on 99 nodes, "
                        f"keep={keep} noise={noise}", "runs": []}
-    for Q in (65536, 262144):
+    for Q in ((65536,) if prof else (65536, 262144)):
         batches = [{k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, Q, s).items()}
                    for s in range(2)]
         t0 = time.time()
@@ -47,7 +61,7 @@ def run(keep, noise):
         for b in batches:
             bn.infer(target, b, N_max=d)
         torch.cuda.synchronize()
-        K = 20
+        K = 10 if prof else 20
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for i in range(K):
@@ -58,7 +72,14 @@ def run(keep, noise):
         plan = next(iter(bn.engine._plans.values()))
         lib = bn.engine._fast[(target, tuple(batches[0].keys()), d)].lib if bn.engine._fast else None
         byt = Q * (4 * len(names) + 4 * d)
-        r = dict(queries=Q, factors=len(plan.factors), us_per_call=round(t * 1e6, 1), queries_per_s=round(Q / t, 1),
+        gather = Q * len(plan.factors) * 4 * d  # one N-float row per factor and query
+        g_tbs = gather / t / 1e12
+        r = dict(label="headline (finite products)" if keep > 0.9 else
+                 "DEGENERATE: every product underflows, all marginals NaN (as the reference)",
+                 roofline=dict(bound="L2/MALL row gather", achieved_TBps=round(g_tbs, 2),
+                               peak_l2_shared_rows_TBps=16.8, peak_mall_random_rows_TBps=8.6,
+                               frac_of_l2_peak=round(g_tbs / 16.8, 3), gather_bytes_per_call=gather),
+                 queries=Q, factors=len(plan.factors), us_per_call=round(t * 1e6, 1), queries_per_s=round(Q / t, 1),
                  effective_GBps=round(byt / t / 1e9, 1), image_MB=round(lib.cbn_plan_table_bytes(plan.handle) / 1e6, 1)
                  if lib else None, fast_path=bool(lib.cbn_plan_max_words(plan.handle)) if lib else None,
                  first_call_s=round(plan_s, 2), fit_s=round(fit_s, 1), nonzero_frac=float((pdf > 0).float().mean()),
