@@ -126,8 +126,12 @@ __device__ __forceinline__ float exp_split(float x) {
     const float pl = fmaf(x, kLlo, fmaf(x, kL, -ph));
     float r = __builtin_amdgcn_exp2f(ph);
     // ph + 64 is exact -- and must not be contracted into fma(x, kL, 64), whose
-    // different rounding pl would not correct
-    if (ph < -126.f) r = __builtin_amdgcn_exp2f(ph + 64.f) * 0x1p-64f;
+    // different rounding pl would not correct.  A wave-uniform branch: the
+    // second transcendental runs only when some lane needs it
+    if (__builtin_expect(__any(ph < -126.f), 0)) {
+        const float rs = __builtin_amdgcn_exp2f(ph + 64.f) * 0x1p-64f;
+        r = ph < -126.f ? rs : r;
+    }
     return fmaf(r, pl * kLn2, r);
 }
 
@@ -151,9 +155,11 @@ __device__ __forceinline__ f2 exp_split2(f2 x) {
     const f2 ph = x * f2s(kL);
     const f2 pl = fma2(x, f2s(kLlo), fma2(x, f2s(kL), -ph));
     f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
-    if (fminf(ph.x, ph.y) < -126.f) {  // subnormal results (see exp_split)
-        if (ph.x < -126.f) r.x = __builtin_amdgcn_exp2f(ph.x + 64.f) * 0x1p-64f;
-        if (ph.y < -126.f) r.y = __builtin_amdgcn_exp2f(ph.y + 64.f) * 0x1p-64f;
+    if (__builtin_expect(__any(fminf(ph.x, ph.y) < -126.f), 0)) {  // subnormal results (see exp_split)
+        const float sx = __builtin_amdgcn_exp2f(ph.x + 64.f) * 0x1p-64f;
+        const float sy = __builtin_amdgcn_exp2f(ph.y + 64.f) * 0x1p-64f;
+        r.x = ph.x < -126.f ? sx : r.x;
+        r.y = ph.y < -126.f ? sy : r.y;
     }
     return fma2(r, pl * f2s(kLn2), r);
 }
