@@ -983,7 +983,9 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     float* simg = reinterpret_cast<float*>(smem4);
     const int T = (nf + 2) >> 1;  // steps: slots 0 .. 2T-1 cover factors 0 .. nf-1 for both orders
     const int S = (T + 1) >> 1;   // step pairs (one int4 of offsets each)
-    const int nsl = 4 * S;        // offset slots per query (past the last factor: ones rows)
+    // offset slots per query (past the last factor: ones rows), plus one
+    // padding pair: the product loop's prefetch reads it unconditionally
+    const int nsl = 4 * (S + 1);
     int* offs = reinterpret_cast<int*>(simg + image_floats);  // [2][kSR][nsl]
     float* wmax = reinterpret_cast<float*>(offs + 2 * kSR * nsl);
     const int tid = threadIdx.x;
@@ -1172,21 +1174,20 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         int4 on = *reinterpret_cast<const int4*>(my);
         load_step(on.x, on.y, A0, A1, A2, A3);
         load_step(on.z, on.w, B0, B1, B2, B3);
-        if (S > 1) on = *reinterpret_cast<const int4*>(my + 4);
+        on = *reinterpret_cast<const int4*>(my + 4);  // pair 1 (the padding pair when S == 1)
         CBN_STAMP(4);
 #ifdef CBN_ABL_NOPROD
         mul_step(A0, A1, A2, A3);
 #else
+        // unconditional prefetch (the padding pair S holds ones rows): no
+        // phi copies of the row registers in the loop
 #pragma unroll 1
         for (int sp = 0; sp < S; ++sp) {  // wave-uniform
             mul_step(A0, A1, A2, A3);
-            const bool more = sp + 1 < S;
-            if (more) load_step(on.x, on.y, A0, A1, A2, A3);
+            load_step(on.x, on.y, A0, A1, A2, A3);
             mul_step(B0, B1, B2, B3);
-            if (more) {
-                load_step(on.z, on.w, B0, B1, B2, B3);
-                if (sp + 2 < S) on = *reinterpret_cast<const int4*>(my + 4 * (sp + 2));
-            }
+            load_step(on.z, on.w, B0, B1, B2, B3);
+            on = *reinterpret_cast<const int4*>(my + 4 * min(sp + 2, S));
         }
 #endif
         CBN_STAMP(5);
@@ -1869,7 +1870,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             P->fast = true;
             P->vpl = vpl;
             P->paired = paired && vpl == 2 && P->use_lds;
-            const size_t st_bytes = img_bytes + (size_t)2 * kSR * (n_factors + 4) * 4 + (kQueryThreads / kWave) * 4 + 64;
+            const int st_T = (n_factors - P->prefix + 2) >> 1, st_S = (st_T + 1) >> 1;  // k_query_staged's nsl
+            const size_t st_bytes =
+                img_bytes + (size_t)2 * kSR * (4 * (st_S + 1)) * 4 + (kQueryThreads / kWave) * 4 + 64;
             if (P->paired && (n_factors - P->prefix) * kFastObs <= kFastPtrsSmall && st_bytes <= (size_t)kLdsBudget &&
                 !getenv("CBN_NO_STAGED")) {
                 P->staged = true;
