@@ -1170,18 +1170,39 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
             r2 = *reinterpret_cast<const float4*>(simg + ob + clo);
             r3 = *reinterpret_cast<const float4*>(simg + ob + chi);
         };
+        // the loop's first rows and offsets are read through volatile pointers:
+        // otherwise the compiler folds them with the loop's own prefetch loads
+        // (phi of loads -> load of phi) and the prefetch sinks to the top of the
+        // next iteration, where nothing overlaps its latency
+        typedef float vf4 __attribute__((ext_vector_type(4)));
+        typedef const volatile __attribute__((address_space(3))) vf4 lds_vf4;
+        auto vld = [&](int o) {
+            const vf4 v = *(lds_vf4*)(simg + o);
+            return make_float4(v.x, v.y, v.z, v.w);
+        };
+        auto vload_step = [&](int oa, int ob, float4& r0, float4& r1, float4& r2, float4& r3) {
+            r0 = vld(oa + clo);
+            r1 = vld(oa + chi);
+            r2 = vld(ob + clo);
+            r3 = vld(ob + chi);
+        };
         float4 A0, A1, A2, A3, B0, B1, B2, B3;
         int4 on = *reinterpret_cast<const int4*>(my);
-        load_step(on.x, on.y, A0, A1, A2, A3);
-        load_step(on.z, on.w, B0, B1, B2, B3);
-        on = *reinterpret_cast<const int4*>(my + 4);  // pair 1 (the padding pair when S == 1)
+        vload_step(on.x, on.y, A0, A1, A2, A3);
+        vload_step(on.z, on.w, B0, B1, B2, B3);
+        {
+            typedef int vi4 __attribute__((ext_vector_type(4)));
+            typedef const volatile __attribute__((address_space(3))) vi4 lds_vi4;
+            const vi4 v = *(lds_vi4*)(my + 4);  // pair 1 (padding when S == 1)
+            on = make_int4(v.x, v.y, v.z, v.w);
+        }
         CBN_STAMP(4);
 #ifdef CBN_ABL_NOPROD
         mul_step(A0, A1, A2, A3);
 #else
         // unconditional prefetch (the padding pair S holds ones rows): no
         // phi copies of the row registers in the loop
-#pragma unroll 1
+#pragma unroll 2
         for (int sp = 0; sp < S; ++sp) {  // wave-uniform
             mul_step(A0, A1, A2, A3);
             load_step(on.x, on.y, A0, A1, A2, A3);
