@@ -1268,9 +1268,19 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         CBN_STAMP(9);
         maxv = wmax[0];
         if (fq >= 0) {
+            // acc / max correctly rounded, as the IEEE division (bayesian_network.py:296),
+            // in ~4 VALU slots instead of ~10: (float)((double)acc * RN64(1 / max)).
+            // The fp64 product is within 2^-52 of acc / max, while a quotient of
+            // two 24-bit significands is either a float or at least 2^-49 (relative)
+            // away from every midpoint between floats, so the final rounding is the
+            // correct one; 0, inf, NaN and subnormal operands give the IEEE results.
+            const double y = 1.0 / (double)maxv;
+            float o[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (float)((double)acc[i] * y);
             const int ob = (int)(fq - q0) * (N * 4);
-            store_wt(orsrc, ob + clo * 4, make_float4(acc[0] / maxv, acc[1] / maxv, acc[2] / maxv, acc[3] / maxv));
-            store_wt(orsrc, ob + chi * 4, make_float4(acc[4] / maxv, acc[5] / maxv, acc[6] / maxv, acc[7] / maxv));
+            store_wt(orsrc, ob + clo * 4, make_float4(o[0], o[1], o[2], o[3]));
+            store_wt(orsrc, ob + chi * 4, make_float4(o[4], o[5], o[6], o[7]));
         }
         CBN_STAMP(10);
     }
