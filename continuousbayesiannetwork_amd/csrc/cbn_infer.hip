@@ -208,7 +208,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, long lo
 }
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
     u32x4_t x = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);  // aux 16 = sc1
+#ifndef CBN_STORE_AUX
+#define CBN_STORE_AUX 16
+#endif
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, CBN_STORE_AUX);  // aux 16 = sc1
 }
 
 // Four ints through the constant address space: at a wave-uniform address that

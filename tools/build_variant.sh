@@ -9,7 +9,8 @@ tmp=$(mktemp -d)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -mllvm -amdgpu-kernarg-preload-count=16 -Wno-unused-result -I include"
 /opt/rocm/bin/hipcc $F "$@" -c -o $tmp/a.o continuousbayesiannetwork_amd/csrc/cbn_infer.hip &
 /opt/rocm/bin/hipcc $F "$@" -c -o $tmp/b.o continuousbayesiannetwork_amd/csrc/cbn_param.hip &
-wait %1 && wait %2
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $tmp/a.o $tmp/b.o
+/opt/rocm/bin/hipcc $F "$@" -c -o $tmp/c.o continuousbayesiannetwork_amd/csrc/cbn_direct.hip &
+wait %1 && wait %2 && wait %3
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $tmp/a.o $tmp/b.o $tmp/c.o
 rm -rf $tmp
 echo "built $out"
