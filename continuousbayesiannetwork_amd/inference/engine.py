@@ -65,6 +65,12 @@ class Plan:
     max_bits: Optional[torch.Tensor] = None
     tables_built: bool = False
     direct: bool = False  # factors evaluated from the CPDs (cbn_plan_create_direct)
+    # BruteForce plans read their sample points through device index arrays
+    # (per factor: node [N], parents [k, N]) that the plan only points at: a
+    # plan whose domains are redrawn every call (N > |domain|) is kept and
+    # those arrays are overwritten in place before each call (tables rebuilt)
+    idx_bufs: list = field(default_factory=list)
+    reusable: bool = False
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -220,6 +226,7 @@ class InferenceEngine:
                 nidx = domain_index(spec.node_samples, doms[-1])
                 keep.append(nidx)
                 d.node_sample_idx = nidx.data_ptr()
+                pidx = None
                 if spec.parents:
                     pidx = torch.zeros((len(spec.parents), N), dtype=torch.int32, device=device)
                     for i, p in enumerate(spec.parents):
@@ -227,6 +234,7 @@ class InferenceEngine:
                             pidx[i] = domain_index(spec.free_samples[p], doms[i])
                     keep.append(pidx)
                     d.parent_sample_idx = pidx.data_ptr()
+                plan.idx_bufs.append((nidx, pidx))
                 for i, p in enumerate(spec.parents):
                     d.parent_card[i] = int(doms[i].numel())
                     if p in spec.observed:
@@ -242,6 +250,7 @@ class InferenceEngine:
             _native.check(rc, "cbn_plan_create")
         plan.handle = handle
         plan.keep = keep
+        plan.reusable = True
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
 
     def _materialise_direct(self, plan: Plan, device: torch.device):
@@ -283,6 +292,7 @@ class InferenceEngine:
                 nidx = domain_index(spec.node_samples, doms[-1])
                 keep.append(nidx)
                 d.node_sample_idx = nidx.data_ptr()
+                pidx = None
                 if k:
                     ev = (ctypes.c_int32 * k)(*[slot_of[p] if p in spec.observed else -1 for p in spec.parents])
                     keep.append(ev)
@@ -293,6 +303,7 @@ class InferenceEngine:
                             pidx[i] = domain_index(spec.free_samples[p], doms[i])
                     keep.append(pidx)
                     d.parent_sample_idx = pidx.data_ptr()
+                plan.idx_bufs.append((nidx, pidx))
             handle = ctypes.c_void_p()
             torch.cuda.current_stream(device).synchronize()  # index arrays ready before the plan reads them
             _native.check(lib.cbn_plan_create_direct(descs, len(plan.factors), N, ctypes.byref(handle)),
@@ -300,6 +311,7 @@ class InferenceEngine:
         plan.handle = handle
         plan.keep = keep
         plan.direct = True
+        plan.reusable = True
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
 
     def _materialise_param(self, plan: Plan, device: torch.device):
@@ -360,6 +372,11 @@ class InferenceEngine:
         if p is not None:
             return p
         order, specs, tdom, det = build_factor_specs(self.bn, target, observed, N)
+        if not det:
+            q = self._plans.get(("redrawn",) + key)
+            if q is not None:
+                self._refresh_indices(q, specs, tdom)
+                return q
         slots = sorted({o for s in specs for o in s.observed})
         if len(slots) > CBN_MAX_EVIDENCE:
             raise _native.NativeError(f"{len(slots)} observed columns > {CBN_MAX_EVIDENCE}")
@@ -368,7 +385,23 @@ class InferenceEngine:
         self._materialise(p, device)
         if det:
             self._plans[key] = p
+        elif p.reusable:
+            self._plans[("redrawn",) + key] = p
         return p
+
+    def _refresh_indices(self, plan: Plan, specs: List[FactorSpec], tdom: torch.Tensor):
+        """This call's redrawn sample points (node.py:302-333) into a kept
+        plan's index arrays (stream-ordered after its previous launches); the
+        tables / constant rows are rebuilt by the next launch."""
+        for (nidx, pidx), spec in zip(plan.idx_bufs, specs):
+            doms = self.bn.nodes_obj[spec.node].estimator.domains
+            nidx.copy_(domain_index(spec.node_samples, doms[-1]))
+            for i, p in enumerate(spec.parents):
+                if p in spec.free_samples:
+                    pidx[i].copy_(domain_index(spec.free_samples[p], doms[i]))
+        plan.factors = specs
+        plan.target_domain = tdom
+        plan.tables_built = False
 
     # --------------------------------------------------------------- infer --
     def _order(self, target: str) -> List[str]:
@@ -396,7 +429,8 @@ class InferenceEngine:
         observed = relevant_observed(self.bn, self._order(target), evidence.keys())
         plan = self.plan(target, observed, N_max, device)
         if not plan.deterministic:
-            plan.destroy()
+            if not plan.reusable:  # (a kept redrawn-domain plan stays cached)
+                plan.destroy()
             raise NotImplementedError(
                 "sharded inference needs N_max <= |domain| for every sampled variable: the reference pads "
                 "larger domains with per-call random values (node.py:302-333) that ranks cannot share")
@@ -426,7 +460,7 @@ class InferenceEngine:
                 self._fast[key] = _FastPath(plan, device, next(iter(evidence)) if len(evidence) else None)
             return res
         finally:
-            if not plan.deterministic:
+            if not plan.deterministic and not plan.reusable:
                 torch.cuda.current_stream(device).synchronize()
                 plan.destroy()
 
@@ -506,7 +540,8 @@ class InferenceEngine:
             observed = relevant_observed(self.bn, self._order(target), evidence.keys())
             plan = self.plan(target, observed, N_max, device)
             if not plan.deterministic:
-                plan.destroy()
+                if not plan.reusable:
+                    plan.destroy()
                 return None
             fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
         return fp if fp.words is not None else None

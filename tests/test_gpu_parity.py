@@ -570,3 +570,26 @@ def test_grid_fast_path_beyond_64_factors(gpu):
     for o, sc in zip(rows, scales):
         sc(o, m)
     np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), a.cpu().numpy())
+
+
+def test_redrawn_domains_reuse_one_plan(gpu):
+    """N_max above a domain's size: the reference pads it with new random
+    values on every call (node.py:302-333).  The engine keeps ONE plan per
+    (target, observed set, N) and rewrites its sample-index arrays in place
+    per call; every call still matches the oracle drawn with the same seed
+    (table plan and direct plan)."""
+    data, cols, edges = chain_data(6, 4, 4000, 21)
+    ora = OracleBN(edges, cols, data)
+    for force_direct in (False, True):
+        bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+        bn.engine.force_direct = force_direct
+        ev = sample_evidence(data, cols, ["X4", "X2"], 200, 6)
+        for seed in (1, 2, 3, 2):
+            random.seed(seed)
+            ref, rdom = ora.infer("X5", ev, 7)
+            random.seed(seed)
+            pdf, dom = bn.infer("X5", _t(ev, gpu), N_max=7)
+            np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
+            np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+        kept = [k for k in bn.engine._plans if k[0] == "redrawn"]
+        assert len(kept) == 1 and len(bn.engine._plans) == 1
