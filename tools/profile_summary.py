@@ -57,6 +57,28 @@ def read_stats(d: str):
     return rows, path
 
 
+def timed_window(d: str, warmup: int, steps: int):
+    """Per-kernel duration stats over the bench's timed region only: dispatches
+    warmup .. warmup + steps - 1 of each kernel in the --kernel-trace CSV (the
+    --stats table also averages the warm-up and the cold-table steps)."""
+    path = find(d, "kernel_trace.csv") if d else None
+    if not path:
+        return {}
+    per = {}
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            per.setdefault(short_name(r["Kernel_Name"]), []).append(
+                (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    out = {}
+    for k, v in per.items():
+        v.sort()
+        x = sorted(t for _, t in v[warmup:warmup + steps])
+        if len(x) >= steps // 2 and x:
+            out[k] = {"timed_dispatches": len(x), "timed_avg_us": round(sum(x) / len(x), 3),
+                      "timed_median_us": x[len(x) // 2], "timed_min_us": x[0], "timed_max_us": x[-1]}
+    return out
+
+
 def pmc_avg(d: str, counter: str):
     """Per-kernel average of one counter over its dispatches (KB, rocprofv3 units)."""
     path = find(d, "counter_collection.csv") if d else None
@@ -79,6 +101,8 @@ def main():
     ap.add_argument("--prof", default=os.path.join(ROOT, "gpurun_out", "prof"))
     ap.add_argument("--fetch", default=os.path.join(ROOT, "gpurun_out", "pmc_fetch"))
     ap.add_argument("--write", default=os.path.join(ROOT, "gpurun_out", "pmc_write"))
+    ap.add_argument("--warmup", type=int, default=20, help="bench warm-up steps before the timed region")
+    ap.add_argument("--steps", type=int, default=200, help="bench timed steps")
     ap.add_argument("--command", default="", help="the profiled command line (recorded in the summary)")
     a = ap.parse_args()
 
@@ -95,6 +119,7 @@ def main():
                 w.writerow(r)
         print("wrote", out_csv)
 
+    timed = timed_window(a.prof, a.warmup, a.steps)
     fetch = pmc_avg(a.fetch, "FETCH_SIZE")
     write = pmc_avg(a.write, "WRITE_SIZE")
     kernels = {}
@@ -102,6 +127,8 @@ def main():
         k = short_name(r["Name"])
         e = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
              "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3}
+        if k in timed and k.startswith("k_query"):
+            e.update(timed[k])
         if k in fetch:
             e["fetch_size_kb"] = fetch[k][0]
             e["fetch_dispatches"] = fetch[k][1]
