@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "cbn_internal.h"
@@ -974,6 +975,12 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 constexpr int kSR = 256;  // queries per block round
 constexpr int kSQ = 128;  // queries per staging unit (two per lane)
 constexpr int kSU = 4;    // staging units per wave per round (nf <= 32 -> nf * 2 / 16 <= 4)
+#ifndef CBN_DMA_WAVES
+#define CBN_DMA_WAVES 4  // A/B on the headline (tools/ab_libs.sh): 1: 15.7, 2: 11.4, 3: 10.35, 4: 10.1, 8: 10.5-11.3, 12: 12.1 us; not split: 10.3 us
+#endif
+constexpr int kDmaW = CBN_DMA_WAVES;                 // round 0: waves issuing the image's LDS-DMA
+constexpr int kEvW = kQueryThreads / kWave - kDmaW;  // round 0: waves staging the evidence
+constexpr int kSUp = (64 + kEvW - 1) / kEvW;         // round 0: units per evidence wave
 
 template <int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
@@ -1007,19 +1014,24 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // (argument block) are wave-uniform scalar loads, all issued before the
     // first is used.  Tags: kTagNone (no observed parent: a dummy column, row
     // 0), kTagMore (further parents, rare: loaded in stage_store).
-    float x[kSU][2] = {};
-    auto stage_load = [&](long long qr) {
+    // Unit k of a wave = u = gw + k * GW (gw: the wave's index in a group of
+    // GW waves that stages a round; KSU * GW >= 64 >= nunits).  Round 0 is
+    // staged by the kEvW evidence waves alone (KSU = kSUp) while the other
+    // waves issue the image's LDS-DMA; later rounds by all 16 waves (kSU).
+    float x[kSUp][2] = {};
+    auto stage_load = [&](long long qr, auto ksu, int gw, int GW) {
+        constexpr int KSU = decltype(ksu)::value;
         // (unconditional: u / 2 < 32 stays inside the table whatever nf is, so
         // these scalar loads do not wait for the scalar arguments)
-        uintptr_t pk[kSU];
+        uintptr_t pk[KSU];
 #pragma unroll
-        for (int k = 0; k < kSU; ++k) {
-            const int u = wid + k * (kQueryThreads / kWave);
-            pk[k] = reinterpret_cast<uintptr_t>(fp.p[(u / (kSR / kSQ)) * kFastObs]);
+        for (int k = 0; k < KSU; ++k) {
+            const int u = gw + k * GW;
+            pk[k] = reinterpret_cast<uintptr_t>(fp.p[((u / (kSR / kSQ)) & 31) * kFastObs]);
         }
 #pragma unroll
-        for (int k = 0; k < kSU; ++k) {
-            const int u = wid + k * (kQueryThreads / kWave);
+        for (int k = 0; k < KSU; ++k) {
+            const int u = gw + k * GW;
             if (u < nunits) {  // wave-uniform
                 const float* col = reinterpret_cast<const float*>(pk[k] & ~(kTagMore | kTagNone));
 #pragma unroll
@@ -1034,17 +1046,18 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // zero row of the factor's bank half) -> offs[buf][query][slot]; non-dense
     // domains binary-search the sorted domain in the image's L2 copy (the LDS
     // copy may not have landed yet)
-    auto stage_store = [&](long long qr, int buf) {
+    auto stage_store = [&](long long qr, int buf, auto ksu, int gw, int GW) {
+        constexpr int KSU = decltype(ksu)::value;
         int* ob = offs + buf * kSR * nsl;
-        int4 rk[kSU];  // {table_off, n_obs, card[0], card[1]} of each unit's factor: all loads issued first
+        int4 rk[KSU];  // {table_off, n_obs, card[0], card[1]} of each unit's factor: all loads issued first
 #pragma unroll
-        for (int k = 0; k < kSU; ++k) {
-            const int u = wid + k * (kQueryThreads / kWave);
+        for (int k = 0; k < KSU; ++k) {
+            const int u = gw + k * GW;
             rk[k] = sload_int4(grec + (u < nunits ? u / (kSR / kSQ) : 0));
         }
 #pragma unroll
-        for (int k = 0; k < kSU; ++k) {
-            const int u = wid + k * (kQueryThreads / kWave);
+        for (int k = 0; k < KSU; ++k) {
+            const int u = gw + k * GW;
             if (u < nunits) {
                 const int f = u / (kSR / kSQ);
                 const int n_obs = rk[k].y, c0 = rk[k].z;
@@ -1114,15 +1127,27 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // evidence loads first, then the image's LDS-DMA: both latencies overlap
     // (a wave's vector-memory counter drains in issue order, so loads issued
     // after the DMA could not be consumed before it lands)
+    // Round 0, warp-specialised: waves [0, kDmaW) issue the image's LDS-DMA at
+    // once (its address is a preloaded argument), waves [kDmaW, 16) load and
+    // stage the evidence (their column pointers are kernel arguments beyond the
+    // preloaded ones: a memory round trip before the first load can issue).
+    // Each wave's vector-memory counter then holds only its own kind of load,
+    // so staging never waits for the DMA and the DMA never waits for the
+    // argument fetch.
     long long qr = q0;
+    const bool dma_wave = wid < kDmaW;  // wave-uniform
+    if (!dma_wave) {
 #ifndef CBN_ABL_NOSTAGE
-    if (qr < q1) stage_load(qr);
+        if (qr < q1) stage_load(qr, std::integral_constant<int, kSUp>{}, wid - kDmaW, kEvW);
 #endif
+    } else {
 #ifndef CBN_ABL_NODMA
-    lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + zero/ones rows + domains + records
+        lds_dma_copy(gimage, smem4, image_floats / 4, kDmaW);  // tables + zero/ones rows + domains + records
 #endif
+    }
     CBN_STAMP(1);
-    if (qr < q1) stage_store(qr, 0);  // (CBN_ABL_NOSTAGE: x uninitialised, offsets still in range)
+    if (!dma_wave && qr < q1)  // (CBN_ABL_NOSTAGE: x uninitialised, offsets still in range)
+        stage_store(qr, 0, std::integral_constant<int, kSUp>{}, wid - kDmaW, kEvW);
     CBN_STAMP(2);
     __syncthreads();  // image landed (vmcnt(0) of the DMA) + round 0 offsets
     CBN_STAMP(3);
@@ -1148,7 +1173,7 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     for (; qr < q1; qr += kSR, buf ^= 1) {  // block-uniform
         const long long qn = qr + kSR;
         // next round's evidence flies during these products (the fused launch has one round)
-        if (MODE != kModeFused && qn < q1) stage_load(qn);
+        if (MODE != kModeFused && qn < q1) stage_load(qn, std::integral_constant<int, kSU>{}, wid, kQueryThreads / kWave);
         const int ql = wid * 16 + qi;
         const long long q = qr + ql;
         const int* my = offs + buf * kSR * nsl + ql * nsl;
@@ -1233,7 +1258,7 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
                 for (int i = 0; i < 8; ++i) lmax = fmaxf(lmax, acc[i]);
         }
         if (MODE != kModeFused && qn < q1) {
-            stage_store(qn, buf ^ 1);
+            stage_store(qn, buf ^ 1, std::integral_constant<int, kSU>{}, wid, kQueryThreads / kWave);
             __syncthreads();  // next round's offsets visible; this round's buffer free
         }
     }

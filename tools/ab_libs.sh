@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of library variants on the headline bench: tools/ab_libs.sh name1 name2 ...
 # (name "base" = the default library; else continuousbayesiannetwork_amd/libcbn_amd_<name>.so);
-# kernel-only rocprof average of k_query_staged<2> per variant, two rounds
+# kernel-only rocprof average of k_query_staged<2> per variant + the bench's HIP-event
+# launch time (no profiler), two rounds
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
@@ -18,5 +19,7 @@ for r in csv.DictReader(open(f)):
         print("$v", "avg", round(float(r["AverageNs"]) / 1000, 2), "us  min", round(float(r["MinNs"]) / 1000, 2))
 PY
   rm -rf gpurun_out/ab_$v
+  CBN_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 400 > gpurun_out/abb_$v.log 2>&1 || exit $?
+  python -c "import json; d=json.loads(open('gpurun_out/abb_$v.log').read().strip().splitlines()[-1]); print('$v', 'bench', round(d['value']/1e9, 3), 'G q/s', d['roofline']['avg_us'], 'us/launch (HIP events)')"
 done
 done
