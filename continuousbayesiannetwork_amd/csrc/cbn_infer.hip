@@ -243,23 +243,6 @@ __device__ __forceinline__ void lds_dma_copy(const float* __restrict__ g, float4
     }
 }
 
-// The chunks [c_lo, c_hi) of the same copy, issued by the waves gw = 0 .. GW-1
-// of a wave group (the staged kernel splits the fill between its DMA waves and,
-// behind their evidence loads, the evidence waves).
-__device__ __forceinline__ void lds_dma_copy_range(const float* __restrict__ g, float4* lds, int n4, int c_lo,
-                                                   int c_hi, int gw, int GW) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int nchunk = (n4 + kWave - 1) / kWave;
-    const int span = c_hi - c_lo;
-    for (int c0 = gw; c0 < span; c0 += GW) {
-        const int c = c_lo + (c0 + (int)blockIdx.x) % span;
-        const int i = c * kWave + lane;
-        if (c < nchunk && i < n4 && CBN_OK_OR(i >= 0, 0))
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)(g + (size_t)i * 4), (lds_void_t*)(lds + c * kWave), 16,
-                                             0, 0);
-    }
-}
-
 // ---------------------------------------------------------------- fit ------
 __global__ void k_cpd_scatter(const int32_t* __restrict__ cell, const float* __restrict__ prob,
                               long long n_rows, float* __restrict__ cpd) {
@@ -995,9 +978,6 @@ constexpr int kSU = 4;    // staging units per wave per round (nf <= 32 -> nf * 
 #ifndef CBN_DMA_WAVES
 #define CBN_DMA_WAVES 4  // A/B on the headline (tools/ab_libs.sh): 1: 15.7, 2: 11.4, 3: 10.35, 4: 10.1, 8: 10.5-11.3, 12: 12.1 us; not split: 10.3 us
 #endif
-#ifndef CBN_DMA_SPLIT
-#define CBN_DMA_SPLIT 16
-#endif
 constexpr int kDmaW = CBN_DMA_WAVES;                 // round 0: waves issuing the image's LDS-DMA
 constexpr int kEvW = kQueryThreads / kWave - kDmaW;  // round 0: waves staging the evidence
 constexpr int kSUp = (64 + kEvW - 1) / kEvW;         // round 0: units per evidence wave
@@ -1154,23 +1134,15 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     // Each wave's vector-memory counter then holds only its own kind of load,
     // so staging never waits for the DMA and the DMA never waits for the
     // argument fetch.
-    // (CBN_DMA_SPLIT / 16 of the image's chunks go to the DMA waves, the rest
-    // to the evidence waves behind their evidence loads)
     long long qr = q0;
     const bool dma_wave = wid < kDmaW;  // wave-uniform
-    const int n4img = image_floats / 4;
-    const int c_split = (((n4img + kWave - 1) / kWave) * CBN_DMA_SPLIT + 15) / 16;
     if (!dma_wave) {
 #ifndef CBN_ABL_NOSTAGE
         if (qr < q1) stage_load(qr, std::integral_constant<int, kSUp>{}, wid - kDmaW, kEvW);
 #endif
-#ifndef CBN_ABL_NODMA
-        if (CBN_DMA_SPLIT < 16)
-            lds_dma_copy_range(gimage, smem4, n4img, c_split, (n4img + kWave - 1) / kWave, wid - kDmaW, kEvW);
-#endif
     } else {
 #ifndef CBN_ABL_NODMA
-        lds_dma_copy_range(gimage, smem4, n4img, 0, c_split, wid, kDmaW);  // tables + zero/ones rows + domains + records
+        lds_dma_copy(gimage, smem4, image_floats / 4, kDmaW);  // tables + zero/ones rows + domains + records
 #endif
     }
     CBN_STAMP(1);

@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 out=continuousbayesiannetwork_amd/libcbn_amd_$name.so
 tmp=$(mktemp -d)
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -mllvm -amdgpu-kernarg-preload-count=16 -Wno-unused-result -I include"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -mllvm -amdgpu-kernarg-preload-count=${PRELOAD:-16} -Wno-unused-result -I include"
 C=continuousbayesiannetwork_amd/csrc
 /opt/rocm/bin/hipcc $F "$@" -c -o $tmp/a.o ${SRC:-$C/cbn_infer.hip}
 for t in cbn_param cbn_direct; do

@@ -55,3 +55,11 @@ late = np.argsort(e)[-8:]
 print("latest-entering blocks:", late.tolist(), (e[late] - t0).tolist())
 grp = np.array([e[b::8].min() - t0 for b in range(8)])
 print("first block entry per b % 8 group:", grp.tolist())
+# prologue by wave role (staged kernel: waves 0..3 issue the image DMA, 4..15 stage the evidence)
+for name, ws in (("DMA waves 0-3", slice(0, 4)), ("evidence waves 4-15", slice(4, 16))):
+    sub = full[:nb, ws, :].reshape(-1, S)
+    parts = []
+    for k in (1, 2, 3):
+        d = sub[:, k] - sub[:, k - 1]
+        parts.append(f"d{k} p50 {np.median(d):.0f} p90 {np.percentile(d, 90):.0f}")
+    print(f"  {name:20s}", " | ".join(parts), f"| entry->sync p50 {np.median(sub[:, 3] - sub[:, 0]):.0f}")
