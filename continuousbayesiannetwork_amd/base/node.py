@@ -85,13 +85,32 @@ class Node:
             return domain_values[idx.to(domain_values.device)]
         if N == card:
             return domain_values
+        out, _ = self._sample_points(node, N)
+        return out.to(domain_values.device)
+
+    def _sample_points(self, node: str, N: int) -> Tuple[torch.Tensor, bool]:
+        """sample_domain's points, consuming ``random`` identically; for
+        N > |domain| they are built on the host ((points, True)) -- the engine
+        maps a redrawn plan's points to domain indices there and uploads only
+        the indices -- otherwise (sample_domain(node, N), False)."""
+        min_value, max_value, _, domain_values = self.info[node]
+        card = domain_values.shape[0]
+        if N <= card:
+            return self.sample_domain(node, N), False
         needed = N - card
-        lo = min_value.detach().to("cpu", torch.float32)
-        span = max_value.detach().to("cpu", torch.float32) - lo
+        # host copies of min, max - min and the domain, cached per info entry:
+        # device reads on every redraw would be a stream sync per node per call
+        cache = self.__dict__.setdefault("_span_cache", {})
+        hit = cache.get(node)
+        if hit is None or hit[0] is not min_value or hit[1] is not max_value or hit[2] is not domain_values:
+            lo = min_value.detach().to("cpu", torch.float32)
+            hit = cache[node] = (min_value, max_value, domain_values, lo,
+                                 max_value.detach().to("cpu", torch.float32) - lo, domain_values.detach().cpu())
+        lo, span, host_dom = hit[3], hit[4], hit[5]
         new_values = torch.stack([lo + span * random.random() for _ in range(needed)])
-        out = torch.cat([domain_values, new_values.to(dtype=domain_values.dtype, device=domain_values.device)])
+        out = torch.cat([host_dom, new_values.to(dtype=host_dom.dtype)])
         out, _ = torch.sort(out)
-        return out
+        return out, True
 
     @staticmethod
     def sample_domain_is_deterministic(info_entry, N: int) -> bool:

@@ -59,7 +59,7 @@ struct DevDirect {
     const int* node_sample_idx;
     DevCpd cpd;
     int cidx;                // constant factors: row of the plan's const buffer
-    int pad;
+    int qk;                  // QUERY factors: row of the per-call key buffer (k_direct_keys)
     DevDCol col[kMaxDP];
 };
 
@@ -72,6 +72,10 @@ struct DirectPlan {
     int* d_cfac = nullptr;      // [n_const]: factor of each const row
     int n_const = 0;
     int max_slots = 0;
+    int nq = 0;                 // QUERY factors
+    int* d_qf = nullptr;        // [nq]: factor of each key row
+    long long* d_keys = nullptr;  // [nq][Q] observed-parent key of each (factor, query), -1: off-domain
+    long long keys_cap = 0;     // elements
 };
 
 }  // namespace cbn
@@ -212,10 +216,40 @@ struct DEv {
     const float* p[CBN_MAX_EVIDENCE];
 };
 
+// Observed-parent part of each QUERY factor's CPD key, once per (factor,
+// query) instead of once per (query, sample column): thread per (k, q), q
+// fastest (coalesced evidence reads, wave-uniform factor).  keys[k * Q + q] =
+// sum over observed parents of domain index * stride, or -1 when a value is
+// outside the fitted domain.
+__global__ void __launch_bounds__(kDThreads) k_direct_keys(const DevDirect* __restrict__ fac,
+                                                            const int* __restrict__ qf, int nq, DEv ev, long long Q,
+                                                            long long* __restrict__ keys) {
+    const long long n = (long long)nq * Q;
+    for (long long it = blockIdx.x * (long long)blockDim.x + threadIdx.x; it < n;
+         it += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(it / Q);
+        const long long q = it - (long long)k * Q;
+        const DevDirect& d = fac[qf[k]];
+        long long base = 0;
+        bool ok = true;
+        for (int p = 0; p < d.n_parents; ++p) {
+            const DevDCol& col = d.col[p];
+            if (col.ev_slot >= 0) {
+                const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
+                ok &= idx >= 0;
+                base += (long long)(idx < 0 ? 0 : idx) * col.stride;
+            }
+        }
+        keys[it] = ok ? base : -1;
+    }
+}
+
 // one thread per (query, sample column): the product over factors in the
-// reference's order; unnormalised rows + one max word per block
+// reference's order; unnormalised rows + one max word per block.  keys: the
+// k_direct_keys rows (nullptr: the observed parents are looked up here)
 __global__ void __launch_bounds__(kDThreads) k_query_direct(const DevDirect* __restrict__ fac, int nf, int N,
                                                              const float* __restrict__ cst, DEv ev, long long Q,
+                                                             const long long* __restrict__ keys,
                                                              unsigned* __restrict__ words, int n_words,
                                                              float* __restrict__ out) {
     const long long n = Q * N;
@@ -234,12 +268,18 @@ __global__ void __launch_bounds__(kDThreads) k_query_direct(const DevDirect* __r
                 const int ni = d.node_sample_idx[j];
                 long long base = ni < 0 ? 0 : ni;
                 bool ok = ni >= 0;
-                for (int p = 0; p < d.n_parents; ++p) {
-                    const DevDCol& col = d.col[p];
-                    if (col.ev_slot >= 0) {
-                        const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
-                        ok &= idx >= 0;
-                        base += (long long)(idx < 0 ? 0 : idx) * col.stride;
+                if (keys) {
+                    const long long kb = keys[(long long)d.qk * Q + q];
+                    ok &= kb >= 0;
+                    base += kb < 0 ? 0 : kb;
+                } else {
+                    for (int p = 0; p < d.n_parents; ++p) {
+                        const DevDCol& col = d.col[p];
+                        if (col.ev_slot >= 0) {
+                            const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
+                            ok &= idx >= 0;
+                            base += (long long)(idx < 0 ? 0 : idx) * col.stride;
+                        }
                     }
                 }
                 x = ok ? direct_free_mean(d, base, N) / (float)d.free_combos : 0.f;
@@ -297,6 +337,8 @@ void cbn::direct_destroy(DirectPlan* dp) {
     if (dp->d_fac) (void)hipFree(dp->d_fac);
     if (dp->d_const) (void)hipFree(dp->d_const);
     if (dp->d_cfac) (void)hipFree(dp->d_cfac);
+    if (dp->d_qf) (void)hipFree(dp->d_qf);
+    if (dp->d_keys) (void)hipFree(dp->d_keys);
     delete dp;
 }
 
@@ -327,13 +369,33 @@ int cbn::direct_run(cbn_plan* plan, int64_t n_queries, const float* const* evide
         const int rc = direct_build_consts(dp, s);
         if (rc) return rc;
     }
+    // observed-parent keys once per (factor, query) when N > 1 columns would
+    // repeat the lookups (the buffer only grows; hipFree waits for the launches
+    // still reading the old one; beyond 256 MiB the query kernel looks the
+    // keys up itself)
+    long long* keys = nullptr;
+    const long long nkeys = (long long)dp->nq * n_queries;
+    if (dp->nq > 0 && dp->N > 1 && nkeys * (long long)sizeof(long long) <= (256LL << 20)) {
+        if (nkeys > dp->keys_cap) {
+            if (dp->d_keys) DHIP_TRY(hipFree(dp->d_keys));
+            dp->d_keys = nullptr;
+            dp->keys_cap = 0;
+            DHIP_TRY(hipMalloc(reinterpret_cast<void**>(&dp->d_keys), sizeof(long long) * nkeys));
+            dp->keys_cap = nkeys;
+        }
+        keys = dp->d_keys;
+        const long long kg = std::max(1LL, std::min((nkeys + kDThreads - 1) / kDThreads, 8LL * num_cu()));
+        hipLaunchKernelGGL(k_direct_keys, dim3((unsigned)kg), dim3(kDThreads), 0, s, dp->d_fac, dp->d_qf, dp->nq, ev,
+                           (long long)n_queries, keys);
+        DHIP_TRY(hipGetLastError());
+    }
     const long long n = n_queries * (long long)dp->N;
     long long grid = (n + kDThreads - 1) / kDThreads;
     grid = std::max(1LL, std::min(grid, (long long)dp->max_slots));
     const bool raw = (flags & CBN_RUN_RAW) != 0;
     unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
     hipLaunchKernelGGL(k_query_direct, dim3((unsigned)grid), dim3(kDThreads), 0, s, dp->d_fac, dp->nf, dp->N,
-                       dp->d_const, ev, (long long)n_queries, words, dp->max_slots, out);
+                       dp->d_const, ev, (long long)n_queries, keys, words, dp->max_slots, out);
     DHIP_TRY(hipGetLastError());
     if (raw) return CBN_OK;
     if (reinterpret_cast<uintptr_t>(out) % 16) return set_err(CBN_E_ARG, "cbn_plan_run: out must be 16-B aligned");
@@ -428,12 +490,19 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
         if ((h.kind == CBN_FACTOR_QUERY) != (d.n_obs > 0)) return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
         if (h.kind != CBN_FACTOR_QUERY) d.cidx = n_const++;
     }
+    std::vector<int> qf;
+    for (int f = 0; f < n_factors; ++f)
+        if (host[f].kind == CBN_FACTOR_QUERY) {
+            host[f].qk = (int)qf.size();
+            qf.push_back(f);
+        }
     DirectPlan* dp = new DirectPlan();
     dp->nf = n_factors;
     dp->ns = ns;
     dp->N = N;
     dp->n_const = n_const;
     dp->max_slots = std::min(4 * num_cu(), kMaxSlots);
+    dp->nq = (int)qf.size();
     std::vector<int> cfac;
     for (int f = 0; f < n_factors; ++f)
         if (host[f].kind != CBN_FACTOR_QUERY) cfac.push_back(f);
@@ -445,10 +514,13 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
     bool ok = hipMalloc(&dp->d_fac, sizeof(DevDirect) * n_factors) == hipSuccess &&
               hipMalloc(&dp->d_const, sizeof(float) * std::max(1, n_const * N)) == hipSuccess &&
               hipMalloc(&dp->d_cfac, sizeof(int) * std::max(1, n_const)) == hipSuccess &&
+              hipMalloc(&dp->d_qf, sizeof(int) * std::max<size_t>(1, qf.size())) == hipSuccess &&
               hipMalloc(&P->d_sync, sizeof(unsigned) * kSyncWords) == hipSuccess;
     ok = ok && hipMemcpy(dp->d_fac, host.data(), sizeof(DevDirect) * n_factors, hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && (cfac.empty() ||
                 hipMemcpy(dp->d_cfac, cfac.data(), sizeof(int) * cfac.size(), hipMemcpyHostToDevice) == hipSuccess);
+    ok = ok && (qf.empty() ||
+                hipMemcpy(dp->d_qf, qf.data(), sizeof(int) * qf.size(), hipMemcpyHostToDevice) == hipSuccess);
     ok = ok && hipMemset(P->d_sync, 0, sizeof(unsigned) * kSyncWords) == hipSuccess;
     if (!ok) {
         cbn_plan_destroy(P);

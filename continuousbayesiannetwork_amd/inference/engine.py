@@ -71,6 +71,8 @@ class Plan:
     # those arrays are overwritten in place before each call (tables rebuilt)
     idx_bufs: list = field(default_factory=list)
     reusable: bool = False
+    host_doms: Optional[list] = None  # redrawn plans: host copies of each factor's estimator domains
+    host_pidx: Optional[list] = None  # ... and of its parent index arrays
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -105,16 +107,23 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
         for p in parents:
             if p in free:
                 deterministic &= nd.sample_domain_is_deterministic(nd.info[p], N)
-                free_samples[p] = nd.sample_domain(p, N)
+                free_samples[p] = nd._sample_points(p, N)[0]  # (redrawn points stay on the host)
         deterministic &= nd.sample_domain_is_deterministic(nd.info[n], N)
-        node_samples = nd.sample_domain(n, N)
+        node_samples, on_host = nd._sample_points(n, N)
         kind = CBN_FACTOR_SCALAR if not parents else (CBN_FACTOR_QUERY if obs else CBN_FACTOR_SHARED)
         specs.append(FactorSpec(n, kind, parents, obs, free_samples, node_samples))
         if n == target:
-            target_dom = node_samples
+            target_dom = node_samples.to(nd.info[n][3].device) if on_host else node_samples
     # bayesian_network.py:265-267 draws the target domain once more (shape only)
-    bn.nodes_obj[target].sample_domain(target, N)
+    bn.nodes_obj[target]._sample_points(target, N)
     return order, specs, target_dom, deterministic
+
+
+def domain_index_host(values: torch.Tensor, domain: torch.Tensor) -> torch.Tensor:
+    """domain_index on host tensors (CPU int32)."""
+    values = values.to(dtype=domain.dtype).contiguous()
+    i = torch.searchsorted(domain, values).clamp_(max=domain.numel() - 1)
+    return torch.where(domain[i] == values, i, torch.full_like(i, -1)).to(torch.int32)
 
 
 class _FastPath:
@@ -393,12 +402,20 @@ class InferenceEngine:
         """This call's redrawn sample points (node.py:302-333) into a kept
         plan's index arrays (stream-ordered after its previous launches); the
         tables / constant rows are rebuilt by the next launch."""
-        for (nidx, pidx), spec in zip(plan.idx_bufs, specs):
-            doms = self.bn.nodes_obj[spec.node].estimator.domains
-            nidx.copy_(domain_index(spec.node_samples, doms[-1]))
-            for i, p in enumerate(spec.parents):
-                if p in spec.free_samples:
-                    pidx[i].copy_(domain_index(spec.free_samples[p], doms[i]))
+        # indices computed on the host against cached host copies of the
+        # estimators' domains (valid for the plan's lifetime: a refit drops
+        # the plan), then one upload per index array
+        if plan.host_doms is None:  # (first refresh: also a host mirror of the parent index arrays)
+            plan.host_doms = [[d.detach().cpu() for d in self.bn.nodes_obj[spec.node].estimator.domains]
+                              for spec in specs]
+            plan.host_pidx = [None if p is None else p.cpu() for _, p in plan.idx_bufs]
+        for (nidx, pidx), spec, hd, hp in zip(plan.idx_bufs, specs, plan.host_doms, plan.host_pidx):
+            nidx.copy_(domain_index_host(spec.node_samples.cpu(), hd[-1]))
+            if pidx is not None and spec.free_samples:
+                for i, p in enumerate(spec.parents):
+                    if p in spec.free_samples:
+                        hp[i] = domain_index_host(spec.free_samples[p].cpu(), hd[i])
+                pidx.copy_(hp)
         plan.factors = specs
         plan.target_domain = tdom
         plan.tables_built = False
