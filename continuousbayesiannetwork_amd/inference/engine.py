@@ -66,13 +66,15 @@ class Plan:
     tables_built: bool = False
     direct: bool = False  # factors evaluated from the CPDs (cbn_plan_create_direct)
     # BruteForce plans read their sample points through device index arrays
-    # (per factor: node [N], parents [k, N]) that the plan only points at: a
-    # plan whose domains are redrawn every call (N > |domain|) is kept and
-    # those arrays are overwritten in place before each call (tables rebuilt)
-    idx_bufs: list = field(default_factory=list)
+    # (per factor: node [N], parents [k, N]; views of idx_flat) that the plan
+    # only points at: a plan whose domains are redrawn every call
+    # (N > |domain|) is kept and those arrays are overwritten in place before
+    # each call (tables rebuilt)
     reusable: bool = False
     host_doms: Optional[list] = None  # redrawn plans: host copies of each factor's estimator domains
-    host_pidx: Optional[list] = None  # ... and of its parent index arrays
+    idx_flat: Optional[torch.Tensor] = None  # every factor's sample-index arrays, one device buffer
+    idx_offs: list = field(default_factory=list)  # per factor: (offset in idx_flat, number of parents)
+    idx_host: Optional[torch.Tensor] = None  # redrawn plans: host mirror of idx_flat
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -220,6 +222,8 @@ class InferenceEngine:
         keep = []
         slot_of = {v: i for i, v in enumerate(plan.slots)}
         N = plan.n_samples
+        self._alloc_index_arrays(plan, device)
+        keep.append(plan.idx_flat)
         with torch.cuda.device(device):
             for f, spec in enumerate(plan.factors):
                 est = self.bn.nodes_obj[spec.node].estimator
@@ -232,18 +236,10 @@ class InferenceEngine:
                 d.n_parents = len(spec.parents)
                 d.node_card = int(doms[-1].numel())
                 d.cpd = cpd.data_ptr() if spec.kind != CBN_FACTOR_SCALAR else est.node_marginal.data_ptr()
-                nidx = domain_index(spec.node_samples, doms[-1])
-                keep.append(nidx)
+                nidx, pidx = self._index_arrays(plan, f, doms, 0)
                 d.node_sample_idx = nidx.data_ptr()
-                pidx = None
-                if spec.parents:
-                    pidx = torch.zeros((len(spec.parents), N), dtype=torch.int32, device=device)
-                    for i, p in enumerate(spec.parents):
-                        if p in spec.free_samples:
-                            pidx[i] = domain_index(spec.free_samples[p], doms[i])
-                    keep.append(pidx)
+                if pidx is not None:
                     d.parent_sample_idx = pidx.data_ptr()
-                plan.idx_bufs.append((nidx, pidx))
                 for i, p in enumerate(spec.parents):
                     d.parent_card[i] = int(doms[i].numel())
                     if p in spec.observed:
@@ -273,6 +269,8 @@ class InferenceEngine:
         keep = []
         slot_of = {v: i for i, v in enumerate(plan.slots)}
         N = plan.n_samples
+        self._alloc_index_arrays(plan, device)
+        keep.append(plan.idx_flat)
         with torch.cuda.device(device):
             for f, spec in enumerate(plan.factors):
                 est = self.bn.nodes_obj[spec.node].estimator
@@ -298,21 +296,13 @@ class InferenceEngine:
                     ref, host = est.cpd_ref()
                 d.cpd = ref
                 keep += [host, est.cpd, est.hash_keys, est.hash_vals, est.node_marginal, *doms]
-                nidx = domain_index(spec.node_samples, doms[-1])
-                keep.append(nidx)
+                nidx, pidx = self._index_arrays(plan, f, doms, -1)
                 d.node_sample_idx = nidx.data_ptr()
-                pidx = None
                 if k:
                     ev = (ctypes.c_int32 * k)(*[slot_of[p] if p in spec.observed else -1 for p in spec.parents])
                     keep.append(ev)
                     d.parent_ev_slot = ctypes.cast(ev, ctypes.POINTER(ctypes.c_int32))
-                    pidx = torch.full((k, N), -1, dtype=torch.int32, device=device)
-                    for i, p in enumerate(spec.parents):
-                        if p in spec.free_samples:
-                            pidx[i] = domain_index(spec.free_samples[p], doms[i])
-                    keep.append(pidx)
                     d.parent_sample_idx = pidx.data_ptr()
-                plan.idx_bufs.append((nidx, pidx))
             handle = ctypes.c_void_p()
             torch.cuda.current_stream(device).synchronize()  # index arrays ready before the plan reads them
             _native.check(lib.cbn_plan_create_direct(descs, len(plan.factors), N, ctypes.byref(handle)),
@@ -398,6 +388,39 @@ class InferenceEngine:
             self._plans[("redrawn",) + key] = p
         return p
 
+    @staticmethod
+    def _alloc_index_arrays(plan: Plan, device):
+        """One flat int32 device buffer for every factor's sample-index arrays
+        (node [N], parents [k, N]): a redrawn plan refreshes all of them with
+        one upload per call."""
+        N = plan.n_samples
+        plan.idx_offs, off = [], 0
+        for spec in plan.factors:
+            plan.idx_offs.append((off, len(spec.parents)))
+            off += N * (1 + len(spec.parents))
+        plan.idx_flat = torch.empty(max(1, off), dtype=torch.int32, device=device)
+        plan.idx_host = None
+
+    @staticmethod
+    def _index_views(flat: torch.Tensor, off: int, k: int, N: int):
+        nidx = flat[off:off + N]
+        return nidx, (flat[off + N:off + N * (1 + k)].view(k, N) if k else None)
+
+    def _index_arrays(self, plan: Plan, f: int, doms, pfill: int):
+        """Factor f's index arrays (views of plan.idx_flat), filled: the node's
+        sample points -> domain index, free parents' likewise, other parent
+        rows ``pfill``."""
+        spec = plan.factors[f]
+        off, k = plan.idx_offs[f]
+        nidx, pidx = self._index_views(plan.idx_flat, off, k, plan.n_samples)
+        nidx.copy_(domain_index(spec.node_samples, doms[-1]))
+        if pidx is not None:
+            pidx.fill_(pfill)
+            for i, p in enumerate(spec.parents):
+                if p in spec.free_samples:
+                    pidx[i] = domain_index(spec.free_samples[p], doms[i])
+        return nidx, pidx
+
     def _refresh_indices(self, plan: Plan, specs: List[FactorSpec], tdom: torch.Tensor):
         """This call's redrawn sample points (node.py:302-333) into a kept
         plan's index arrays (stream-ordered after its previous launches); the
@@ -405,17 +428,18 @@ class InferenceEngine:
         # indices computed on the host against cached host copies of the
         # estimators' domains (valid for the plan's lifetime: a refit drops
         # the plan), then one upload per index array
-        if plan.host_doms is None:  # (first refresh: also a host mirror of the parent index arrays)
+        if plan.host_doms is None:  # (first refresh: also a host mirror of the flat index buffer)
             plan.host_doms = [[d.detach().cpu() for d in self.bn.nodes_obj[spec.node].estimator.domains]
                               for spec in specs]
-            plan.host_pidx = [None if p is None else p.cpu() for _, p in plan.idx_bufs]
-        for (nidx, pidx), spec, hd, hp in zip(plan.idx_bufs, specs, plan.host_doms, plan.host_pidx):
-            nidx.copy_(domain_index_host(spec.node_samples.cpu(), hd[-1]))
-            if pidx is not None and spec.free_samples:
-                for i, p in enumerate(spec.parents):
-                    if p in spec.free_samples:
-                        hp[i] = domain_index_host(spec.free_samples[p].cpu(), hd[i])
-                pidx.copy_(hp)
+            plan.idx_host = plan.idx_flat.cpu()
+        N = plan.n_samples
+        for (off, k), spec, hd in zip(plan.idx_offs, specs, plan.host_doms):
+            hn, hp = self._index_views(plan.idx_host, off, k, N)
+            hn.copy_(domain_index_host(spec.node_samples.cpu(), hd[-1]))
+            for i, p in enumerate(spec.parents):
+                if p in spec.free_samples:
+                    hp[i] = domain_index_host(spec.free_samples[p].cpu(), hd[i])
+        plan.idx_flat.copy_(plan.idx_host)  # one upload, ordered after the plan's earlier launches
         plan.factors = specs
         plan.target_domain = tdom
         plan.tables_built = False
