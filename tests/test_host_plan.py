@@ -68,3 +68,27 @@ def test_cpu_device_fails_loudly():
     bn = make_bn(BayesianNetwork, m["edges"], m["columns"], g["data"], device="cpu")
     with pytest.raises(RuntimeError, match="HIP device"):
         bn.infer("X4", {"X3": torch.tensor(g["evidence"]["X3"])}, N_max=4)
+
+
+def test_host_sample_points_match_sample_domain():
+    """Node._sample_points (host points of a redrawn domain, engine-internal)
+    consumes ``random`` exactly like sample_domain and gives the same points;
+    domain_index_host == domain_index."""
+    from continuousbayesiannetwork_amd.inference.engine import domain_index, domain_index_host
+    from helpers import chain_data
+
+    data, cols, edges = chain_data(4, 3, 500, 5)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device="cpu")
+    nd = bn.nodes_obj["X2"]
+    for N in (2, 3, 7, 16):
+        random.seed(11)
+        a = nd.sample_domain("X2", N)
+        ra = random.random()
+        random.seed(11)
+        b, on_host = nd._sample_points("X2", N)
+        rb = random.random()
+        assert on_host == (N > 3)
+        assert ra == rb
+        assert torch.equal(a.cpu(), b.cpu())
+        dom = nd.info["X2"][3]
+        assert torch.equal(domain_index(b, dom).cpu(), domain_index_host(b.cpu(), dom.cpu()))
