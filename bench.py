@@ -11,12 +11,17 @@ factor-row gather/product, global max, normalised write).  The factor tables
 are plan constants (fitted CPDs x target x observed columns x N, independent
 of evidence values) built once per plan; ``--rebuild-tables`` re-runs that
 build every step, and the default run also reports that figure as
-``value_rebuild_tables``.  N > 1: the batch grows with N (weak scaling), each rank
-owns 65 536 queries and the ranks exchange the global max with one RCCL
-all-reduce of the block max words between the raw launch and the in-place
-scale, pipelined so a step's exchange overlaps the next step's launch
-(distributed.ShardedStepper; ``--serial-exchange`` for the unpipelined step,
-``--sharded`` runs that N>1 step at N=1 over a one-rank RCCL communicator).
+``value_rebuild_tables``.  N > 1 (``--gpus N`` starts N ranks itself through a
+child ``torch.distributed.run`` unless it already runs under one): the batch
+grows with N (weak scaling), each rank owns 65 536 queries and the ranks
+exchange the global max with one RCCL all-reduce of the block max words
+between the raw launch and the in-place scale, pipelined so a step's exchange
+overlaps the next step's launch (distributed.ShardedStepper;
+``--serial-exchange`` for the unpipelined step, ``--sharded`` runs that N>1
+step at N=1 over a one-rank RCCL communicator).  ``value`` keeps every rank's
+normalised rows on that rank (the marginal tensor stays sharded); the step
+with the RCCL all-gather reassembly of the full tensor on every rank is timed
+after it and reported as ``value_gathered`` (``--gather`` swaps the two).
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` for the dominant
 kernel -- the single-launch fused query kernel at N=1 (the write pass when the
@@ -89,13 +94,57 @@ def parse():
                     help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
     ap.add_argument("--exchange-every", type=int, default=8,
                     help="N>1: steps per all-reduce + scale group (1..8)")
-    ap.add_argument("--no-gather", action="store_true",
-                    help="N>1: keep each rank's rows (no all-gather reassembly of the [Q, N] marginal tensor); by "
-                         "default the step includes the reassembly and the rank-local step is reported beside it")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: time the step WITH the all-gather reassembly of the [Q, N] marginal tensor on every "
+                         "rank as `value`; by default each rank keeps its normalised shard of the marginal tensor "
+                         "(the reassembly cannot scale: DESIGN.md, Multi-GPU) and the gathered step is measured "
+                         "after it and reported as value_gathered")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_command(gpus: int, argv, port: int, script: str = None):
+    """The child command that runs this script as ``gpus`` ranks on one node
+    (one process per GPU, torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, env) -> int:
+    """World size this process runs in; --gpus and WORLD_SIZE must agree when
+    both are given (a torch.distributed.run launch with a different rank count
+    would time the wrong number of GPUs)."""
+    w = env.get("WORLD_SIZE")
+    if w is None:
+        return 1
+    if int(w) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={w} (launch with matching rank count)")
+    return int(w)
+
+
+def launch_ranks(a, argv) -> int:
+    """``--gpus N > 1`` outside torch.distributed.run: start the N ranks as a
+    CHILD process (never exec: nothing here has touched the GPU, and the
+    parent only waits) and return its exit code."""
+    import subprocess
+
+    cmd = rank_launch_command(a.gpus, argv, free_port())
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between the rank processes)
+    print("bench.py: launching", " ".join(cmd), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 _ORACLE = None  # per-worker OracleBN of the CPU baseline pool
@@ -155,7 +204,9 @@ def cpu_baseline(data, cols, edges, ev_np, target, N, budget_s):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, sys.argv[1:]))  # N ranks as a child torch.distributed.run
+    world = check_world(a.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sharded = world > 1 or a.sharded
@@ -192,7 +243,7 @@ def main():
     # of the block max words + the in-place scale run on a comm stream, once per
     # --exchange-every steps (8) for all of them, so the exchange overlaps the next steps' launches
     # (distributed.ShardedStepper)
-    gather = sharded and not a.no_gather
+    gather = sharded and a.gather
     stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
                              force_exchange=sharded, gather=gather)
 
@@ -316,16 +367,18 @@ def main():
                         avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_step, timed_steps=K,
                         timing="HIP events on rank 0's launch stream around the timed region / K steps")
 
-    local = None
-    if sharded and gather:
-        # the same step without the reassembly (each rank keeps its rows), for reference
+    other = None
+    if sharded:
+        # the same step with the other reassembly choice, for reference: the
+        # all-gather of the full [Q, N] tensor on every rank (value_gathered), or
+        # (with --gather) each rank keeping its rows (value_rank_local)
         stepper.close()
         stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                                 force_exchange=True, gather=False)
+                                 force_exchange=True, gather=not gather)
         for _ in range(a.warmup):
             step()
         stepper.wait()
-        local = Q * world * K / timed_steps(K)
+        other = Q * world * K / timed_steps(K)
 
     cold = None
     if not sharded and not a.rebuild_tables:
@@ -360,10 +413,12 @@ def main():
         }
         if cold is not None:
             line["value_rebuild_tables"] = round(cold, 1)
-        if local is not None:
-            line["value_rank_local"] = round(local, 1)  # same step, each rank keeps its own rows (no all-gather)
+        if other is not None:
+            # same step, each rank keeps its own rows / every rank all-gathers the full tensor
+            line["value_gathered" if not gather else "value_rank_local"] = round(other, 1)
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        assert line["n_gpus"] == a.gpus, (line["n_gpus"], a.gpus)
         print(json.dumps(line), flush=True)
     if sharded:
         stepper.close()

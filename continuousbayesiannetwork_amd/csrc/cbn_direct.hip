@@ -3,7 +3,7 @@
 //
 // Reference: BayesianNetwork.infer (cbn/base/bayesian_network.py:208-305) over
 // factors from Node.get_prob (cbn/base/node.py:115-204) evaluated by
-// BruteForce._get_prob (cbn/parameter_learning/brute_force.py:185-257), which
+// BruteForce._get_prob (cbn/parameter_learning/brute_force.py:172-244), which
 // answers ANY fitted data -- continuous or high-cardinality columns, any
 // number of parents -- with equality scans over the unique training rows.
 //

@@ -1,12 +1,12 @@
 // cbn_infer.hip -- MI355X (gfx950) kernels + C ABI for the batched inference
 // path of ContinuousBayesianNetwork's BayesianNetwork.infer
 // (reference: cbn/base/bayesian_network.py:208-305, cbn/base/node.py:115-375,
-//  cbn/parameter_learning/brute_force.py:30-257).
+//  cbn/parameter_learning/brute_force.py:17-244).
 //
 // Design:
 //   * fit:  the BruteForce maximum-likelihood rows become a dense CPD table per
 //           node (k_cpd_scatter / k_cpd_normalize).  The reference instead scans
-//           all rows with equality masks on every call (brute_force.py:240-254).
+//           all rows with equality masks on every call (brute_force.py:227-241).
 //   * plan: every ancestor factor of the target is marginalised over its free
 //           parents ONCE per call into a small table (k_build_tables):
 //             SCALAR [1], SHARED [N], QUERY [prod(card of observed parents), N].
@@ -257,7 +257,7 @@ __global__ void k_cpd_normalize(float* __restrict__ cpd, long long n_pcells, int
         float* row = cpd + c * card;
         float s = 0.f;
         for (int v = 0; v < card; ++v) s += row[v];
-        const float den = s + 1e-10f;  // brute_force.py:253-254
+        const float den = s + 1e-10f;  // brute_force.py:240-241
         for (int v = 0; v < card; ++v) row[v] = row[v] / den;
     }
 }

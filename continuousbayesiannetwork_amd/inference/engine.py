@@ -283,7 +283,7 @@ class InferenceEngine:
                 d.kind = spec.kind
                 d.n_parents = k
                 if spec.kind == CBN_FACTOR_SCALAR:
-                    # root: the node marginal (brute_force.py:205-214) as a one-column dense CPD
+                    # root: the node marginal (brute_force.py:192-201) as a one-column dense CPD
                     mdoms = (ctypes.c_void_p * 1)(doms[-1].data_ptr())
                     mcards = (ctypes.c_int32 * 1)(int(doms[-1].numel()))
                     ref = _native.CpdRef()

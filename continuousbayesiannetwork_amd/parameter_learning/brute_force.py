@@ -38,7 +38,7 @@ MAX_DENSE_CELLS = 1 << 24  # 64 MiB of fp32 per dense CPD; larger CPDs are hashe
 def sparse_conditionals(cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool) -> torch.Tensor:
     """Value of each unique row of a hashed CPD (cell = mixed-radix domain
     index, node column last): joint / (parent marginal + 1e-10), the sums of
-    brute_force.py:240-254 over the rows sharing the row's parent values; the
+    brute_force.py:227-241 over the rows sharing the row's parent values; the
     root case (:205-214) keeps the joint."""
     if not conditional:
         return probs.clone()
@@ -80,7 +80,7 @@ class BruteForce(BaseParameterLearningEstimator):
 
     # -------------------------------------------------------------- fit ----
     def _fit(self, node_data: torch.Tensor, parents_data: torch.Tensor = None):
-        """brute_force.py:30-66: unique rows + empirical probabilities."""
+        """brute_force.py:17-53: unique rows + empirical probabilities."""
         node_data = node_data.view(-1, 1)
         if parents_data is not None:
             parents_data = parents_data.T
@@ -138,7 +138,7 @@ class BruteForce(BaseParameterLearningEstimator):
                     idx_last = idx
                 cell += idx * stride
                 stride *= cards[c]
-            # P(node value) over all rows: the query=None case of brute_force.py:205-214
+            # P(node value) over all rows: the query=None case of brute_force.py:192-201
             marg = torch.zeros(cards[-1], dtype=torch.float32, device=dev)
             marg.index_add_(0, idx_last, probs)
             if n_cells <= self.dense_limit:
@@ -158,7 +158,7 @@ class BruteForce(BaseParameterLearningEstimator):
 
     def _build_sparse(self, lib, dev, cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool):
         """Hashed CPD: value of unique row u = joint_u / (sum of joint over the
-        rows sharing u's parent values + 1e-10) (brute_force.py:240-254), the
+        rows sharing u's parent values + 1e-10) (brute_force.py:227-241), the
         root case without the division (:205-214)."""
         vals = sparse_conditionals(cell, probs, card_node, conditional)
         n = cell.numel()
@@ -215,7 +215,7 @@ class BruteForce(BaseParameterLearningEstimator):
         return out
 
     def _get_prob(self, point_to_evaluate: torch.Tensor, query: torch.Tensor = None):
-        """brute_force.py:185-257 semantics, evaluated by table lookup."""
+        """brute_force.py:172-244 semantics, evaluated by table lookup."""
         assert self.mle_tensor is not None, "MLE tensor not fitted yet. Call _fit() first."
         n_node_values = point_to_evaluate.shape[1]
         if query is None:
@@ -238,7 +238,7 @@ class BruteForce(BaseParameterLearningEstimator):
         return self.eval_points(full.view(-1, n_parents + 1)).view(n_queries, n_node_values)
 
     def _sample(self, N: int, **kwargs):
-        """brute_force.py:259-278: N rows drawn from the empirical joint."""
+        """brute_force.py:246-265: N rows drawn from the empirical joint."""
         assert self.mle_tensor is not None, "MLE tensor not fitted yet. Call _fit() first."
         probs = self.mle_tensor[:, -1]
         indices = torch.multinomial(probs, N, replacement=True)

@@ -66,8 +66,8 @@ int cbn_abi_version(void);
 const char* cbn_last_error(void);
 
 /* Dense BruteForce CPD from the fitted maximum-likelihood rows.
- * Replaces brute_force.py:30-66 (_fit's mle_tensor) + the per-call equality
- * scans of brute_force.py:240-254 (joint / parent-marginal sums).
+ * Replaces brute_force.py:17-53 (_fit's mle_tensor) + the per-call equality
+ * scans of brute_force.py:227-241 (joint / parent-marginal sums).
  *   cell[r]  : flat index of mle row r in [n_parent_cells, node_card]
  *   prob[r]  : its empirical probability (counts / total)
  *   normalize: 1 -> cpd = joint / (sum_v joint + 1e-10)  (conditional, :253)
@@ -77,7 +77,7 @@ int cbn_bf_cpd_build(const int32_t* cell, const float* prob, int64_t n_rows,
                      float* cpd, void* stream);
 
 /* Evaluate a dense BruteForce CPD at arbitrary float points.
- * Replaces BruteForce._get_prob (brute_force.py:185-257):
+ * Replaces BruteForce._get_prob (brute_force.py:172-244):
  *   points   : [n_points, n_cols] float32, columns = parents..., node
  *   domains  : per column, a sorted domain array (device) and its size
  *   out[i]   : cpd[idx(points[i])], 0 where any value is not in its domain
@@ -90,7 +90,7 @@ int cbn_bf_cpd_eval(const float* cpd, int32_t n_cols, const float* const* domain
  * with more than CBN_MAX_PARENTS parents.
  *
  * The reference answers BruteForce.get_prob for ANY fitted data with two
- * equality scans over the unique training rows (brute_force.py:228-247), so
+ * equality scans over the unique training rows (brute_force.py:228-237), so
  * continuous / high-cardinality columns work there at O(points x rows) per
  * call.  A dense table over the columns' domains would hold prod(cards)
  * cells; past a size limit the estimator keeps instead a hash table keyed by
@@ -119,7 +119,7 @@ typedef struct cbn_cpd_ref {
     int64_t capacity;             /* sparse: slots (power of two)                   */
 } cbn_cpd_ref;
 
-/* BruteForce._get_prob (brute_force.py:185-257) on a dense or hashed CPD:
+/* BruteForce._get_prob (brute_force.py:172-244) on a dense or hashed CPD:
  * out[i] = P(points[i]) -- points [n_points, n_cols] float32. */
 int cbn_cpd_ref_eval(const cbn_cpd_ref* cpd, const float* points, int64_t n_points, float* out, void* stream);
 

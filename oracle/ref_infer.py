@@ -8,8 +8,8 @@ It restates, with numpy (plus torch CPU for the two reference helpers whose
 float32 semantics are torch-specific: ``torch.linspace(...).round()`` and the
 tensor-valued ``random.uniform``), the algorithm of:
 
-* ``cbn/parameter_learning/brute_force.py:30-66``   BruteForce._fit
-* ``cbn/parameter_learning/brute_force.py:185-257`` BruteForce._get_prob
+* ``cbn/parameter_learning/brute_force.py:17-53``   BruteForce._fit
+* ``cbn/parameter_learning/brute_force.py:172-244`` BruteForce._get_prob
 * ``cbn/base/node.py:45-110``   Node.fit (domain bookkeeping in ``info``)
 * ``cbn/base/node.py:115-204``  Node.get_prob
 * ``cbn/base/node.py:206-284``  Node._setup_parents_query
@@ -41,20 +41,20 @@ import networkx as nx
 import numpy as np
 import torch
 
-EPS = np.float32(1e-10)  # brute_force.py:253
+EPS = np.float32(1e-10)  # brute_force.py:240
 
 
 # --------------------------------------------------------------------------
 # BruteForce estimator (brute_force.py)
 # --------------------------------------------------------------------------
 class OracleBruteForce:
-    """brute_force.py:21-283 restated on numpy float32."""
+    """brute_force.py:8-271 restated on numpy float32."""
 
     def __init__(self):
         self.mle = None  # [n_unique, k+2] float32: parents..., node, prob
 
     def fit(self, node_data: np.ndarray, parents_data: Optional[np.ndarray]):
-        # brute_force.py:36-66
+        # brute_force.py:23-53
         node_data = np.asarray(node_data, np.float32).reshape(-1, 1)
         if parents_data is not None:
             pd_ = np.asarray(parents_data, np.float32).T  # [S, k]
@@ -69,12 +69,12 @@ class OracleBruteForce:
         self.mle = mle
 
     def get_prob(self, points: np.ndarray, query: Optional[np.ndarray] = None) -> np.ndarray:
-        """brute_force.py:185-257.  points [Qr, V]; query [Qr, k, 1] or None."""
+        """brute_force.py:172-244.  points [Qr, V]; query [Qr, k, 1] or None."""
         points = np.asarray(points, np.float32)
         mle_data = self.mle[:, :-1]
         mle_probs = self.mle[:, -1]
         if query is None:
-            # brute_force.py:205-214: marginal P(node_value)
+            # brute_force.py:192-201: marginal P(node_value)
             node_values = mle_data[:, -1]
             out = np.zeros_like(points)
             for i in range(points.shape[0]):

@@ -1,6 +1,6 @@
 """Direct inference plans (csrc/cbn_direct.hip) and hashed BruteForce CPDs.
 
-The reference's BruteForce (cbn/parameter_learning/brute_force.py:185-257)
+The reference's BruteForce (cbn/parameter_learning/brute_force.py:172-244)
 answers any fitted data by scanning its unique rows, so networks with > 8
 parents per node, continuous columns and high-cardinality domains all infer.
 Here those plans evaluate every factor per (query, sample column) straight
@@ -82,7 +82,7 @@ def test_forced_hashed_cpds_match_reference(name, gpu):
 
 @pytest.mark.parametrize("dense_limit", [None, 1])
 def test_bruteforce_get_prob_wide_and_hashed(dense_limit, gpu):
-    """BruteForce._get_prob (brute_force.py:185-257) with 11 columns (beyond
+    """BruteForce._get_prob (brute_force.py:172-244) with 11 columns (beyond
     the dense evaluator) and with a hashed CPD, on- and off-domain points."""
     rng = np.random.default_rng(3)
     k = 10

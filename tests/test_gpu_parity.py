@@ -112,7 +112,7 @@ def test_node_get_prob_matches_oracle(gpu):
 
 
 def test_bruteforce_get_prob_matches_oracle(gpu):
-    """BruteForce._get_prob (brute_force.py:185-257) at on- and off-domain points."""
+    """BruteForce._get_prob (brute_force.py:172-244) at on- and off-domain points."""
     from continuousbayesiannetwork_amd import BruteForce
 
     rng = np.random.default_rng(0)

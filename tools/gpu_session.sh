@@ -32,6 +32,8 @@ for s in "$@"; do
     stepper) step pytest_stepper 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "stepper or raw_launch" --timeout 120 --timeout-method thread ;;
     probe) step shard_probe 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 tools/shard_step_probe.py ;;
     benchsharded) step bench_sharded 300 python bench.py --no-cpu-baseline --sharded ;;
+    profsharded) step rocprof_sharded 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sharded" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --sharded ;;
+    bench2) step bench_n2 600 python bench.py --gpus 2 --no-cpu-baseline ;;
     benchserial) step bench_serial 300 python bench.py --no-cpu-baseline --sharded --serial-exchange ;;
     torchrun1) step bench_torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 1 --no-cpu-baseline ;;
     param) step pytest_param 400 python -u -m pytest tests/test_gpu_param.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
