@@ -15,6 +15,18 @@ import torch
 from . import BASE_MAX_CARDINALITY, KEY_CONTINUOUS, KEY_DISCRETE, KEY_MAX_CARDINALITY_FOR_DISCRETE
 from ..utils import choose_probability_estimator
 
+# Source of the uniform draws sample_domain consumes for N > |domain|
+# (node.py:313-317: random.uniform -> random.random()).  None: Python's global
+# ``random``, as the reference.  distributed.shared_draws installs a callable
+# n -> n floats so that every rank of a sharded call uses rank 0's draws.
+_DRAWS = [None]
+
+
+def uniforms(n: int) -> list:
+    """The next n ``random.random()`` values of this process's draw source."""
+    src = _DRAWS[0]
+    return [random.random() for _ in range(n)] if src is None else src(n)
+
 
 class Node:
     def __init__(self, node_name: str, estimator_name: str, parameter_learning_config: Dict,
@@ -107,7 +119,9 @@ class Node:
             hit = cache[node] = (min_value, max_value, domain_values, lo,
                                  max_value.detach().to("cpu", torch.float32) - lo, domain_values.detach().cpu())
         lo, span, host_dom = hit[3], hit[4], hit[5]
-        new_values = torch.stack([lo + span * random.random() for _ in range(needed)])
+        # lo + span * r on 0-dim float32 tensors (random.uniform): r is rounded to
+        # float32 first, then one float32 multiply and one add -- vectorised
+        new_values = lo + span * torch.tensor(uniforms(needed), dtype=torch.float64).to(torch.float32)
         out = torch.cat([host_dom, new_values.to(dtype=host_dom.dtype)])
         out, _ = torch.sort(out)
         return out, True

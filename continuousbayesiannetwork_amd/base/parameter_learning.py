@@ -7,13 +7,16 @@ import torch
 
 # Bumped whenever any estimator's fitted state changes (fit, load_model, a
 # parameter edit followed by _invalidate): inference plans capture raw device
-# pointers to CPDs / packed weights, so the engine drops every cached plan when
-# the generation it was built under is stale (one integer compare per call).
+# pointers to CPDs / packed weights.  One integer compare per call tells an
+# engine that SOME estimator changed; it then compares the stamps of its own
+# network's estimators and drops its cached plans only if one of them moved.
 GENERATION = [0]
 
 
-def bump_generation():
+def bump_generation(estimator=None):
     GENERATION[0] += 1
+    if estimator is not None:
+        estimator._stamp = GENERATION[0]
 
 
 class BaseParameterLearningEstimator(ABC):
@@ -29,7 +32,7 @@ class BaseParameterLearningEstimator(ABC):
     def fit(self, node_data: torch.Tensor, parents_data: torch.Tensor = None):
         """node_data [n_samples]; parents_data [n_parents_features, n_samples]."""
         self._fit(node_data, parents_data)
-        bump_generation()
+        bump_generation(self)
 
     @abstractmethod
     def _fit(self, node_data: torch.Tensor, parents_data: torch.Tensor = None):

@@ -21,8 +21,10 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <array>
 #include <chrono>
+#include <cmath>
 
 #include <cstdint>
 #include <cstring>
@@ -537,9 +539,71 @@ int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max)
                                           reinterpret_cast<const unsigned*>(max_ptr), n_max, s);
 }
 
+// ------------------------------------------------------ redrawn sample domains --
+// A plan whose sample domains are redrawn on every call (N > |domain|: the
+// reference pads the domain with random.uniform draws and sorts, node.py:
+// 302-333) keeps its device plan; per call only its sample-index arrays
+// change.  This computes all of them from the call's uniforms in one host
+// call.  Job j (one sample_domain call, in the reference's order) takes the
+// next need_j values of r, forms lo_j + span_j * float(r) in float32 (what
+// random.uniform does on the 0-dim float32 tensors of Node.info), sorts them
+// together with the variable's domain (torch.sort of the concatenation) and
+// writes the index of every point in the estimator's domain (-1: absent;
+// the BruteForce lookup is by value) to idx[dest_j .. dest_j + N); the
+// target's points also go to pts.
+//   meta  int64 [J, 7]: need, sdom_off, sdom_len, ldom_off, ldom_len, dest (-1: none), want_pts
+//   lospan float32 [J, 2]; doms float32 (flat sample / lookup domains, sorted)
+void redraw(py::list r, const at::Tensor& meta, const at::Tensor& lospan, const at::Tensor& doms, at::Tensor idx,
+            at::Tensor pts, int64_t N) {
+    if (meta.scalar_type() != at::kLong || lospan.scalar_type() != at::kFloat || doms.scalar_type() != at::kFloat ||
+        idx.scalar_type() != at::kInt || !meta.is_contiguous() || !lospan.is_contiguous() || !idx.is_contiguous() ||
+        meta.dim() != 2 || meta.size(1) != 7 || lospan.size(0) != meta.size(0) || meta.is_cuda() || idx.is_cuda())
+        throw std::invalid_argument("redraw: bad job tables");
+    const int64_t J = meta.size(0), R = (int64_t)py::len(r);
+    const int64_t* m = meta.data_ptr<int64_t>();
+    const float* ls = lospan.data_ptr<float>();
+    const float* dm = doms.data_ptr<float>();
+    int32_t* out = idx.data_ptr<int32_t>();
+    const int64_t nidx = idx.numel(), ndoms = doms.numel();
+    std::vector<float> p;
+    int64_t k = 0;
+    for (int64_t j = 0; j < J; ++j, m += 7) {
+        const int64_t need = m[0], soff = m[1], slen = m[2], loff = m[3], llen = m[4], dest = m[5];
+        if (need < 0 || k + need > R || soff < 0 || soff + slen > ndoms || loff < 0 || loff + llen > ndoms ||
+            slen + need != N || (dest >= 0 && dest + N > nidx))
+            throw std::invalid_argument("redraw: job " + std::to_string(j) + " out of range");
+        p.assign(dm + soff, dm + soff + slen);
+        const float lo = ls[2 * j], span = ls[2 * j + 1];
+        for (int64_t i = 0; i < need; ++i) {
+            const float u = (float)PyFloat_AsDouble(PyList_GET_ITEM(r.ptr(), k + i));  // .to(float32): nearest
+            const float t = span * u;  // two rounded float32 operations, as torch does them
+            p.push_back(lo + t);
+        }
+        k += need;
+        if (PyErr_Occurred()) throw py::error_already_set();
+        if (dest < 0 && !m[6]) continue;  // bayesian_network.py:265-267: drawn for its shape only
+        // torch.sort: ascending, NaN last
+        std::sort(p.begin(), p.end(), [](float a, float b) { return std::isnan(b) ? !std::isnan(a) : a < b; });
+        if (m[6]) {
+            if (pts.numel() != N || pts.scalar_type() != at::kFloat || pts.is_cuda())
+                throw std::invalid_argument("redraw: pts must be a host float32 [N] tensor");
+            std::memcpy(pts.data_ptr<float>(), p.data(), sizeof(float) * N);
+        }
+        if (dest < 0) continue;
+        const float* ld = dm + loff;
+        for (int64_t i = 0; i < N; ++i) {
+            const float v = p[i];
+            const float* it = std::lower_bound(ld, ld + llen, v);
+            out[dest + i] = (it != ld + llen && *it == v) ? (int32_t)(it - ld) : -1;
+        }
+    }
+    if (k != R) throw std::invalid_argument("redraw: " + std::to_string(R - k) + " uniforms left over");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.def("redraw", &redraw);
     m.doc() = "cbn MI355X host fast path (cached-plan infer)";
     m.def("run", &run);
     m.def("scale", &scale);

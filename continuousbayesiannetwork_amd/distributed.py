@@ -10,10 +10,14 @@ rank keeps the rows it owns.
 """
 from __future__ import annotations
 
+import random
+from contextlib import contextmanager
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+from .base.parameter_learning import GENERATION
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -66,6 +70,63 @@ def gather_rows(out: torch.Tensor, group=None, total_rows: Optional[int] = None)
     return full
 
 
+@contextmanager
+def shared_draws(group=None):
+    """Every rank of ``group`` uses rank 0's sample_domain draws inside the
+    block (node.py:302-333 pads a domain smaller than N with random.uniform
+    values; a sharded call must use ONE set of them, as the single process
+    does).  Rank 0 draws from its own ``random`` in the reference's order and
+    broadcasts the values when the block ends (also on error, so no rank
+    waits forever); every other rank receives them at its first draw and
+    replays them, and checks it used exactly as many."""
+    from .base import node as node_mod
+
+    rank = dist.get_rank(group)
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    if node_mod._DRAWS[0] is not None:
+        raise RuntimeError("shared_draws blocks do not nest")
+    if rank == 0:
+        rec = []
+
+        def draw(n):
+            v = [random.random() for _ in range(n)]
+            rec.extend(v)
+            return v
+
+        node_mod._DRAWS[0] = draw
+        try:
+            yield
+        finally:
+            node_mod._DRAWS[0] = None
+            dist.broadcast_object_list([rec], src=src, group=group)
+        return
+    st = {"vals": None, "pos": 0}
+
+    def recv():
+        obj = [None]
+        dist.broadcast_object_list(obj, src=src, group=group)
+        st["vals"] = obj[0]
+
+    def draw(n):
+        if st["vals"] is None:
+            recv()
+        v = st["vals"][st["pos"]:st["pos"] + n]
+        if len(v) != n:
+            raise RuntimeError("ranks disagree on the number of sample_domain draws of this call")
+        st["pos"] += n
+        return v
+
+    node_mod._DRAWS[0] = draw
+    try:
+        yield
+    finally:
+        node_mod._DRAWS[0] = None
+        if st["vals"] is None:
+            recv()
+    if st["pos"] != len(st["vals"]):
+        raise RuntimeError("ranks disagree on the number of sample_domain draws of this call")
+
+
 def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor], N_max: int = 16,
                   group=None, gather: bool = False, out: Optional[torch.Tensor] = None):
     """``BayesianNetwork.infer`` over a query batch sharded across ranks.
@@ -76,22 +137,35 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
     Fast-path plans: ONE launch per rank stores the unnormalised rows and the
     rank's max word, RCCL all-reduces the word (MAX), and an in-place scale
     launch divides by the global max.  Other plans: max pass, all-reduce,
-    write pass.
+    write pass.  Plans whose sample domains are redrawn on every call (N_max
+    above a sampled variable's domain size) use rank 0's draws on every rank
+    (``shared_draws``), so every rank's rows are those of the single process.
     """
     eng = bn.engine
     multi = dist.is_initialized() and dist.get_world_size(group) > 1
-    raw = eng.infer_raw(target_node, evidence_shard, N_max, out)
-    if raw is None and multi and eng.raw_fast_path(target_node, evidence_shard, N_max) is not None:
+    if multi and eng.redraws(target_node, evidence_shard.keys(), N_max):
+        with shared_draws(group):
+            plan, fp = eng.call_plan(target_node, evidence_shard, N_max)
+    else:
+        plan, fp = eng.call_plan(target_node, evidence_shard, N_max)
+    try:
+        return _sharded_on_plan(eng, plan, fp, target_node, evidence_shard, N_max, group, gather, out, multi)
+    finally:
+        if not plan.deterministic and not plan.reusable:  # a plan rebuilt per call
+            torch.cuda.current_stream().synchronize()
+            plan.destroy()
+
+
+def _sharded_on_plan(eng, plan, fp, target_node, evidence_shard, N_max, group, gather, out, multi):
+    n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
+    raw = eng.infer_raw(target_node, evidence_shard, N_max, out, fp=fp) if (fp is not None and n > 0) else None
+    if raw is None and multi and fp is not None and fp.words is not None and n == 0:
         # an empty shard on a raw-capable plan: no rows, zero max words -- the
         # same collectives as the other ranks
-        fp = eng.raw_fast_path(target_node, evidence_shard, N_max)
-        n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
-        if n == 0:
-            plan = fp.plan
-            rows = torch.empty((0, plan.n_samples), dtype=torch.float32, device=fp.device)
-            bits = torch.zeros_like(fp.words)
-            raw = (rows, plan.target_domain.unsqueeze(0).expand(0 if plan.target_observed else 1, -1), bits,
-                   lambda r, b: r)
+        rows = torch.empty((0, plan.n_samples), dtype=torch.float32, device=fp.device)
+        bits = torch.zeros_like(fp.words)
+        raw = (rows, plan.target_domain.unsqueeze(0).expand(0 if plan.target_observed else 1, -1), bits,
+               lambda r, b: r)
     # the path must be the same on every rank (different collectives would hang):
     # take the raw path only where every rank can
     ok = torch.tensor([1 if raw is not None else 0], dtype=torch.int32)
@@ -107,9 +181,9 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
         if gather and multi:
             rows = gather_rows(rows, group)
         return rows, tdom
-    if raw is not None:  # this rank launched a raw pass another rank cannot take: redo it two-pass
-        torch.cuda.current_stream().synchronize()
-    plan, cols, nq, tdom, device = eng.prepare(target_node, evidence_shard, N_max)
+    # (a raw pass this rank launched that another rank cannot take is redone
+    # two-pass below, stream-ordered after it)
+    cols, nq, tdom, device = eng.prepare_plan(plan, evidence_shard)
     if out is None:
         out = torch.empty((nq, plan.n_samples), dtype=torch.float32, device=device)
 
@@ -171,6 +245,7 @@ class ShardedStepper:
         self._fp = None
         self._comm = 0
         self._serial = False
+        self._epoch = None  # engine.epoch the native stepper's plan handle belongs to
 
     def _setup(self, evidence_shard) -> bool:
         import ctypes
@@ -178,11 +253,13 @@ class ShardedStepper:
 
         from . import _native
 
-        fp = self.bn.engine.raw_fast_path(self.target, evidence_shard, self.N_max)
+        eng = self.bn.engine
+        fp = eng.raw_fast_path(self.target, evidence_shard, self.N_max)
         if fp is None:
             return False
+        self._epoch = eng.epoch
         host = _native.load_host()
-        if self.exchange:
+        if self.exchange and not self._comm:  # (kept across plan rebuilds)
             rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
             if dist.is_initialized():
                 world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
@@ -204,8 +281,11 @@ class ShardedStepper:
     def _counts(self, n: int, total_rows: Optional[int]):
         if not self.gather:
             return None
-        if total_rows is None:  # equal shards
-            return [n] * self.world
+        if total_rows is None:
+            if self.world > 1:  # every rank's count must be known to size its all-gather: no guessing
+                raise ValueError("ShardedStepper(gather=True).step needs total_rows (the whole batch, split by "
+                                 "shard_bounds) when more than one rank takes part")
+            return [n]
         return [shard_bounds(total_rows, self.world, r)[1] - shard_bounds(total_rows, self.world, r)[0]
                 for r in range(self.world)]
 
@@ -214,8 +294,17 @@ class ShardedStepper:
         """One step on this rank's shard.  ``gather=True``: returns the full
         [Q, N] tensor (Q = ``total_rows``, the whole batch split by
         ``shard_bounds``; None = equal shards), otherwise this rank's rows."""
+        eng = self.bn.engine
+        if GENERATION[0] != eng._gen:
+            eng._check_generation()  # drops this network's plans if one of its estimators changed
+        if self._c is not None and eng.epoch != self._epoch:
+            # the plan the native stepper launches on was destroyed: finish what
+            # was enqueued on it, then rebind to the rebuilt plan (every rank
+            # refits alike, so every rank flushes here at the same step)
+            self._c.synchronize()
+            self._c = self._fp = None
         if self._c is None and not self._serial and not self._setup(evidence_shard):
-            self._serial = True  # the plan has no raw launch: every rank decides alike (plan-level)
+            self._serial = True  # the plan has no raw launch / redraws its domains: every rank decides alike
         if self._serial:
             return sharded_infer(self.bn, self.target, evidence_shard, self.N_max, self.group, gather=self.gather,
                                  out=out)

@@ -75,6 +75,8 @@ class Plan:
     idx_flat: Optional[torch.Tensor] = None  # every factor's sample-index arrays, one device buffer
     idx_offs: list = field(default_factory=list)  # per factor: (offset in idx_flat, number of parents)
     idx_host: Optional[torch.Tensor] = None  # redrawn plans: host mirror of idx_flat
+    redraw: Optional["RedrawProgram"] = None  # redrawn plans: the per-call draws (host_fast.redraw jobs)
+    observed: frozenset = frozenset()  # the observed parent columns the plan was built for
 
     def destroy(self):
         if self.handle is not None and self.handle.value:
@@ -121,6 +123,82 @@ def build_factor_specs(bn, target: str, observed: frozenset, N: int) -> Tuple[Li
     return order, specs, target_dom, deterministic
 
 
+def sample_calls(bn, order: Sequence[str], observed: frozenset):
+    """The sample_domain calls of one infer, in the reference's order (the walk
+    of build_factor_specs, without drawing): (factor index, node, variable,
+    parent position or -1 for the node's own points); the final
+    (-1, target, target, -1) is bayesian_network.py:265-267's shape-only draw."""
+    calls = []
+    for f, n in enumerate(order):
+        parents = list(bn.nodes_obj[n].parents_names)
+        obs = [p for p in parents if p in observed]
+        if parents and obs != parents:
+            calls += [(f, n, p, i) for i, p in enumerate(parents) if p not in obs]
+        calls.append((f, n, n, -1))
+    calls.append((-1, order[-1], order[-1], -1))
+    return calls
+
+
+def needs_redraw(bn, order: Sequence[str], observed: frozenset, N: int) -> bool:
+    """True when some sample_domain call of the infer draws random padding
+    (N > |domain|, node.py:302-333)."""
+    return any(N > bn.nodes_obj[n].info[v][3].shape[0] for _, n, v, _ in sample_calls(bn, order, observed))
+
+
+class RedrawProgram:
+    """host_fast.redraw's job tables for a kept plan whose sample domains are
+    redrawn on every call: one job per drawing sample_domain call, in the
+    reference's order, each writing its sorted points' domain indices into the
+    plan's host index mirror (and, for the target's own points, the returned
+    target domain).  Built once per plan from the fitted domains (a refit
+    drops the plan)."""
+
+    def __init__(self, bn, plan: "Plan", observed: frozenset):
+        N = plan.n_samples
+        meta, lospan, doms, off = [], [], [], 0
+        self.total = 0
+        self.target_pts = False
+        cache = {}
+
+        def flat(t: torch.Tensor):
+            nonlocal off
+            key = id(t)
+            if key not in cache:
+                h = t.detach().to("cpu").contiguous()
+                if h.dtype != torch.float32:
+                    raise TypeError("redraw program needs float32 domains")
+                doms.append(h)
+                cache[key] = (off, h.numel(), t)  # (t kept alive: ids stay unique)
+                off += h.numel()
+            return cache[key][:2]
+
+        for f, n, v, i in sample_calls(bn, plan.order, observed):
+            nd = bn.nodes_obj[n]
+            mn, mx, _, dom = nd.info[v]
+            need = N - dom.shape[0]
+            if need <= 0:
+                continue  # deterministic: fixed in the plan's index arrays
+            lo = mn.detach().to("cpu", torch.float32)
+            span = mx.detach().to("cpu", torch.float32) - lo
+            soff, slen = flat(dom)
+            if f < 0:
+                dest, loff, llen, pts = -1, 0, 0, 0
+            else:
+                est_doms = nd.estimator.domains
+                loff, llen = flat(est_doms[-1] if i < 0 else est_doms[i])
+                foff, _ = plan.idx_offs[f]
+                dest = foff if i < 0 else foff + N * (1 + i)
+                pts = 1 if (i < 0 and n == plan.target) else 0
+                self.target_pts |= bool(pts)
+            meta.append([need, soff, slen, loff, llen, dest, pts])
+            lospan.append([float(lo), float(span)])
+            self.total += need
+        self.meta = torch.tensor(meta, dtype=torch.int64).reshape(-1, 7)
+        self.lospan = torch.tensor(lospan, dtype=torch.float32).reshape(-1, 2)
+        self.doms = torch.cat(doms) if doms else torch.zeros(1)
+        self.pts = torch.empty(N, dtype=torch.float32)
+
+
 def domain_index_host(values: torch.Tensor, domain: torch.Tensor) -> torch.Tensor:
     """domain_index on host tensors (CPU int32)."""
     values = values.to(dtype=domain.dtype).contiguous()
@@ -132,10 +210,11 @@ class _FastPath:
     """Everything the hot path needs for one cached (target, evidence keys, N)."""
 
     __slots__ = ("plan", "device", "first", "ptrs", "max_ptr", "lib", "tdom", "host", "run_fn", "slot_keys",
-                 "scale_fn", "host_scale", "words")
+                 "scale_fn", "host_scale", "words", "redraw")
 
     def __init__(self, plan: "Plan", device: torch.device, first_key):
         self.plan = plan
+        self.redraw = not plan.deterministic  # a kept plan whose sample domains are redrawn on every call
         self.device = device
         self.first = first_key
         self.ptrs = (ctypes.c_void_p * max(1, len(plan.slots)))()
@@ -173,23 +252,37 @@ class InferenceEngine:
         # batch fits one round of the resident grid; False forces two launches
         self.fused = True
         self._fast: Dict[tuple, "_FastPath"] = {}
-        self._gen = GENERATION[0]  # estimator generation the cached plans were built under
+        self._gen = GENERATION[0]  # estimator generation last checked
+        self._sig = self._signature()  # this network's estimator states the cached plans were built under
+        # bumped whenever cached plans are destroyed: holders of raw plan
+        # handles (distributed.ShardedStepper) rebuild when it moved
+        self.epoch = 0
         # evaluate every BruteForce factor from its CPD (direct plans) even when
         # the table path could take the plan (tests; the direct path is chosen
         # by itself for hashed CPDs, > 8 parents and oversized tables)
         self.force_direct = False
 
+    def _signature(self):
+        if not self.bn.nodes_obj:
+            return ()
+        return tuple((id(nd.estimator), getattr(nd.estimator, "_stamp", 0)) for nd in self.bn.nodes_obj.values())
+
     def _check_generation(self):
-        """Drop every cached plan when any estimator was refitted / reloaded /
-        edited since they were built (plans hold raw device pointers to the
-        CPDs and packed weights of that state)."""
+        """Drop every cached plan when an estimator of THIS network was
+        refitted / reloaded / edited (or replaced) since they were built (plans
+        hold raw device pointers to the CPDs and packed weights of that
+        state); another network's refit leaves them."""
         if GENERATION[0] != self._gen:
-            self.invalidate()
+            sig = self._signature()
+            if sig != self._sig:
+                self.invalidate()
+                self._sig = sig
             self._gen = GENERATION[0]
 
     def invalidate(self):
         if self._plans:
             torch.cuda.synchronize()
+        self.epoch += 1
         for p in self._plans.values():
             p.destroy()
         self._plans = {}
@@ -370,22 +463,27 @@ class InferenceEngine:
         p = self._plans.get(key)
         if p is not None:
             return p
+        q = self._plans.get(("redrawn",) + key)
+        if q is not None:
+            self._redraw_plan(q)  # this call's draws
+            return q
         order, specs, tdom, det = build_factor_specs(self.bn, target, observed, N)
-        if not det:
-            q = self._plans.get(("redrawn",) + key)
-            if q is not None:
-                self._refresh_indices(q, specs, tdom)
-                return q
         slots = sorted({o for s in specs for o in s.observed})
         if len(slots) > CBN_MAX_EVIDENCE:
             raise _native.NativeError(f"{len(slots)} observed columns > {CBN_MAX_EVIDENCE}")
         tobs = any(s.observed for s in specs if s.node == target)
         p = Plan(target, int(N), order, specs, slots, tdom, tobs, det)
+        p.observed = observed
         self._materialise(p, device)
         if det:
             self._plans[key] = p
         elif p.reusable:
             self._plans[("redrawn",) + key] = p
+            p.idx_host = p.idx_flat.cpu()  # host mirror: this call's indices; later calls rewrite the drawn ones
+            try:
+                p.redraw = RedrawProgram(self.bn, p, observed)
+            except TypeError:  # non-float32 domains: later calls re-walk build_factor_specs
+                p.redraw = None
         return p
 
     @staticmethod
@@ -421,17 +519,33 @@ class InferenceEngine:
                     pidx[i] = domain_index(spec.free_samples[p], doms[i])
         return nidx, pidx
 
-    def _refresh_indices(self, plan: Plan, specs: List[FactorSpec], tdom: torch.Tensor):
+    def _redraw_plan(self, plan: Plan):
         """This call's redrawn sample points (node.py:302-333) into a kept
-        plan's index arrays (stream-ordered after its previous launches); the
-        tables / constant rows are rebuilt by the next launch."""
-        # indices computed on the host against cached host copies of the
-        # estimators' domains (valid for the plan's lifetime: a refit drops
-        # the plan), then one upload per index array
-        if plan.host_doms is None:  # (first refresh: also a host mirror of the flat index buffer)
+        plan: the call's uniforms drawn in the reference's order
+        (base.node.uniforms), every drawn domain's sorted points mapped to
+        estimator-domain indices in ONE native host call (host_fast.redraw)
+        into the plan's host index mirror, then one upload (stream-ordered after
+        the plan's earlier launches); the tables / constant rows are rebuilt by
+        the next launch."""
+        from ..base.node import uniforms
+
+        rd = plan.redraw
+        if rd is None:
+            return self._refresh_indices_walk(plan)
+        _native.load_host().redraw(uniforms(rd.total), rd.meta, rd.lospan, rd.doms, plan.idx_host, rd.pts,
+                                   plan.n_samples)
+        plan.idx_flat.copy_(plan.idx_host)
+        if rd.target_pts:  # a new tensor per call: earlier results keep their domain
+            plan.target_domain = rd.pts.to(plan.idx_flat.device)
+        plan.tables_built = False
+
+    def _refresh_indices_walk(self, plan: Plan):
+        """_redraw_plan for domains the job tables do not take (not float32):
+        the draws through build_factor_specs, the index maps per factor."""
+        _, specs, tdom, _ = build_factor_specs(self.bn, plan.target, plan.observed, plan.n_samples)
+        if plan.host_doms is None:
             plan.host_doms = [[d.detach().cpu() for d in self.bn.nodes_obj[spec.node].estimator.domains]
                               for spec in specs]
-            plan.idx_host = plan.idx_flat.cpu()
         N = plan.n_samples
         for (off, k), spec, hd in zip(plan.idx_offs, specs, plan.host_doms):
             hn, hp = self._index_views(plan.idx_host, off, k, N)
@@ -439,10 +553,15 @@ class InferenceEngine:
             for i, p in enumerate(spec.parents):
                 if p in spec.free_samples:
                     hp[i] = domain_index_host(spec.free_samples[p].cpu(), hd[i])
-        plan.idx_flat.copy_(plan.idx_host)  # one upload, ordered after the plan's earlier launches
-        plan.factors = specs
+        plan.idx_flat.copy_(plan.idx_host)
         plan.target_domain = tdom
         plan.tables_built = False
+
+    def redraws(self, target: str, evidence_keys, N_max: int) -> bool:
+        """Whether an infer of (target, evidence keys, N) draws random sample
+        points (the same answer on every rank of a sharded call)."""
+        order = self._order(target)
+        return needs_redraw(self.bn, order, relevant_observed(self.bn, order, evidence_keys), N_max)
 
     # --------------------------------------------------------------- infer --
     def _order(self, target: str) -> List[str]:
@@ -462,34 +581,64 @@ class InferenceEngine:
             cols.append(t)
         return cols
 
-    def prepare(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int):
-        """Plan + device evidence columns of one (deterministic) call, without launching."""
+    def call_plan(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int):
+        """(plan, fast path) of one call with the call's sample-domain draws made
+        -- exactly once per call, in the reference's order: a kept plan whose
+        domains are redrawn gets its new points here.  The fast path is None for
+        plans rebuilt per call (the caller destroys those after use)."""
+        key = (target, tuple(evidence.keys()), N_max)
+        if GENERATION[0] != self._gen:
+            self._check_generation()
+        fp = self._fast.get(key)
+        if fp is not None:
+            if fp.redraw:
+                self._redraw(fp)
+            return fp.plan, fp
         device = _native.require_gpu(self.bn.device)
-        evidence.items()
-        n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
         observed = relevant_observed(self.bn, self._order(target), evidence.keys())
         plan = self.plan(target, observed, N_max, device)
-        if not plan.deterministic:
-            if not plan.reusable:  # (a kept redrawn-domain plan stays cached)
-                plan.destroy()
-            raise NotImplementedError(
-                "sharded inference needs N_max <= |domain| for every sampled variable: the reference pads "
-                "larger domains with per-call random values (node.py:302-333) that ranks cannot share")
+        if plan.deterministic or plan.reusable:
+            fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)) if len(evidence) else None)
+            return plan, fp
+        return plan, None
+
+    def _redraw(self, fp: "_FastPath"):
+        self._redraw_plan(fp.plan)
+        fp.tdom.clear()
+
+    def prepare(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int):
+        """Plan (this call's draws made) + device evidence columns of one call,
+        without launching: (plan, cols, n_queries, target domain, device).  A
+        plan rebuilt per call is the caller's to destroy."""
+        plan, _ = self.call_plan(target, evidence, N_max)
+        return (plan, *self.prepare_plan(plan, evidence))
+
+    def prepare_plan(self, plan: Plan, evidence: Dict[str, torch.Tensor]):
+        """Device evidence columns + target domain of one call on ``plan``
+        (two-pass sharded path), without launching."""
+        device = _native.require_gpu(self.bn.device)
+        n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
         cols = self._columns(plan, evidence, n_queries, device)
         tq = n_queries if plan.target_observed else 1
-        return plan, cols, n_queries, plan.target_domain.unsqueeze(0).expand(tq, -1), device
+        return cols, n_queries, plan.target_domain.unsqueeze(0).expand(tq, -1), device
 
     def infer(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int,
               out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        # lean path: (target, evidence keys, N) -> cached deterministic plan
+        # lean path: (target, evidence keys, N) -> cached plan (a kept redrawn
+        # plan draws this call's points first)
         key = (target, tuple(evidence.keys()), N_max)  # evidence=None raises AttributeError, as the reference
         if GENERATION[0] != self._gen:
             self._check_generation()
         fp = self._fast.get(key)
         if fp is not None:
+            if fp.redraw:
+                self._redraw(fp)
             res = self._run_fast(fp, evidence, out)
             if res is not None:
                 return res
+            # conversions / the reference's errors, on the same (already drawn) plan
+            n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
+            return self._run(fp.plan, dict(evidence.items()), n_queries, fp.device, out)
         device = _native.require_gpu(self.bn.device)
         items = evidence.items()
         n_queries = next(iter(evidence.values())).shape[0] if len(evidence) > 0 else 1
@@ -497,7 +646,7 @@ class InferenceEngine:
         plan = self.plan(target, observed, N_max, device)
         try:
             res = self._run(plan, dict(items), n_queries, device, out)
-            if plan.deterministic:
+            if plan.deterministic or plan.reusable:
                 self._fast[key] = _FastPath(plan, device, next(iter(evidence)) if len(evidence) else None)
             return res
         finally:
@@ -506,7 +655,8 @@ class InferenceEngine:
                 plan.destroy()
 
     def infer_raw(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int,
-                  out: Optional[torch.Tensor] = None, words: Optional[torch.Tensor] = None):
+                  out: Optional[torch.Tensor] = None, words: Optional[torch.Tensor] = None,
+                  fp: Optional["_FastPath"] = None):
         """One launch storing this batch's UNnormalised rows (the factor product
         of bayesian_network.py:269-295) and its max word -- the per-rank step of
         the sharded path, which all-reduces the word and then calls the returned
@@ -517,10 +667,13 @@ class InferenceEngine:
         exchange).  The W words are per-block maxima (all-reduce them with MAX).
         ``words``: a caller-owned int32[W] buffer for them (W =
         ``raw_word_count``); by default the plan's own buffer, which the next
-        raw launch of the same plan overwrites.
+        raw launch of the same plan overwrites.  ``fp``: the fast path
+        ``call_plan`` returned for this call (its draws made); by default the
+        cached deterministic one (``raw_fast_path``).
         """
-        fp = self.raw_fast_path(target, evidence, N_max)
         if fp is None:
+            fp = self.raw_fast_path(target, evidence, N_max)
+        if fp is None or fp.words is None:
             return None
         plan = fp.plan
         if words is None:
@@ -568,24 +721,22 @@ class InferenceEngine:
         return rc if rc else out  # (converted copies: stream-ordered frees on the launch stream)
 
     def raw_fast_path(self, target: str, evidence: Dict[str, torch.Tensor], N_max: int) -> Optional["_FastPath"]:
-        """The cached fast path of (target, evidence keys, N) when its plan takes
-        raw launches (planned here if needed, nothing launched); else None."""
+        """The cached fast path of (target, evidence keys, N) when its plan is
+        deterministic and takes raw launches (planned here if needed, nothing
+        launched, nothing drawn); else None.  Plans whose sample domains are
+        redrawn per call go through ``call_plan`` (one draw per call)."""
         key = (target, tuple(evidence.keys()), N_max)
         if GENERATION[0] != self._gen:
             self._check_generation()
         fp = self._fast.get(key)
         if fp is None:
             device = _native.require_gpu(self.bn.device)
-            if len(evidence) == 0:
+            if len(evidence) == 0 or self.redraws(target, evidence.keys(), N_max):
                 return None
             observed = relevant_observed(self.bn, self._order(target), evidence.keys())
             plan = self.plan(target, observed, N_max, device)
-            if not plan.deterministic:
-                if not plan.reusable:
-                    plan.destroy()
-                return None
             fp = self._fast[key] = _FastPath(plan, device, next(iter(evidence)))
-        return fp if fp.words is not None else None
+        return fp if (fp.words is not None and not fp.redraw) else None
 
     def raw_flags(self, plan: Plan) -> int:
         return self._flags(plan) | _native.CBN_RUN_RAW

@@ -77,7 +77,7 @@ class _Parametric(BaseParameterLearningEstimator):
     # ---- packing ----
     def _invalidate(self):
         self._packed = None
-        bump_generation()  # cached inference plans hold the old packed weights
+        bump_generation(self)  # cached inference plans hold the old packed weights
 
     def _scale_norm(self) -> Tuple[float, float]:
         """sigma / s and the Gaussian normaliser as the reference computes them

@@ -234,3 +234,199 @@ def test_step_ring_two_ranks_rank_local(tmp_path):
 def test_step_ring_two_ranks_gather(tmp_path):
     """Same, with the reassembly: every rank ends with the full [Q, N] tensor."""
     _ring_case(tmp_path, 2, gather=True)
+
+
+# ---------------------------------------------------------------------------
+# sharded_infer's collective decisions, world size 2, the oracle as the device
+# ---------------------------------------------------------------------------
+class _LogDist:
+    """torch.distributed as sharded_infer sees it, with every collective logged."""
+
+    def __init__(self, log):
+        self._log = log
+
+    def __getattr__(self, name):
+        f = getattr(dist, name)
+        if name in ("all_reduce", "all_gather", "broadcast_object_list", "broadcast"):
+            def logged(*a, **k):
+                t = a[0]
+                self._log.append([name, list(t.shape) if hasattr(t, "shape") else len(t)])
+                return f(*a, **k)
+            return logged
+        return f
+
+
+class _OracleEngine:
+    """CPU stand-in for InferenceEngine behind sharded_infer: the real host
+    logic decides whether the call redraws sample domains (engine.needs_redraw
+    on a CPU mirror of the network) and consumes the call's draws through the
+    real draw source (base.node.uniforms, i.e. through shared_draws); the
+    oracle computes the rows, its ``random`` replaced by those draws.
+    ``raw_ok``: whether this rank's plan takes a raw launch."""
+
+    def __init__(self, bn, ora, raw_ok):
+        self.bn, self.ora, self.raw_ok = bn, ora, raw_ok
+        self.vals, self.raw = [], None
+
+    def _order(self, target):
+        return self.bn.get_ancestors(self.bn.initial_dag, target) + [target]
+
+    def redraws(self, target, keys, N):
+        from continuousbayesiannetwork_amd.inference.engine import needs_redraw, relevant_observed
+
+        order = self._order(target)
+        return needs_redraw(self.bn, order, relevant_observed(self.bn, order, keys), N)
+
+    def call_plan(self, target, ev, N):
+        from types import SimpleNamespace
+
+        from continuousbayesiannetwork_amd.base.node import uniforms
+        from continuousbayesiannetwork_amd.inference.engine import relevant_observed, sample_calls
+
+        order = self._order(target)
+        obs = relevant_observed(self.bn, order, ev.keys())
+        total = sum(max(0, N - self.bn.nodes_obj[n].info[v][3].shape[0]) for _, n, v, _ in
+                    sample_calls(self.bn, order, obs))
+        self.vals = uniforms(total)  # this call's draws, in the reference's order
+        self.target = target
+        plan = SimpleNamespace(n_samples=N, deterministic=total == 0, reusable=True, target_observed=True,
+                               target_domain=torch.zeros(N))
+        fp = SimpleNamespace(words=torch.zeros(1, dtype=torch.int32) if self.raw_ok else None,
+                             device=torch.device("cpu"), plan=plan)
+        return plan, fp
+
+    def _rows(self, ev, N):
+        it = iter(self.vals)
+        saved = random.random
+        random.random = lambda: next(it)
+        try:
+            raw, dom = self.ora.infer_raw(self.target, {k: v.numpy() for k, v in ev.items()}, N)
+        finally:
+            random.random = saved
+        return torch.tensor(raw), torch.tensor(dom)
+
+    @staticmethod
+    def _bits(rows):
+        m = float(rows.max()) if rows.numel() else 0.0
+        return torch.tensor([np.float32(m).view(np.int32)], dtype=torch.int32)
+
+    @staticmethod
+    def _div(rows, bits):
+        return rows.div_(torch.tensor(np.int32(bits.max().item()).view(np.float32)))
+
+    def infer_raw(self, target, ev, N, out=None, fp=None):
+        if not self.raw_ok:
+            return None
+        rows, dom = self._rows(ev, N)
+        return rows, dom, self._bits(rows), self._div
+
+    def prepare_plan(self, plan, ev):
+        n = next(iter(ev.values())).shape[0]
+        return list(ev.values()), n, torch.zeros((1, plan.n_samples)), torch.device("cpu")
+
+    def query_max(self, plan, cols, nq, device):
+        ev = dict(zip(self._keys, cols))
+        self.raw = self._rows(ev, plan.n_samples)[0] if nq else torch.zeros((0, plan.n_samples))
+        return self._bits(self.raw)
+
+    def query_write(self, plan, cols, nq, bits, out, device):
+        out[:] = self._div(self.raw.clone(), bits)
+        return out
+
+
+import random  # noqa: E402  (used by the stand-in engine)
+
+CASES = {
+    # name: (raw_ok per rank, shard sizes per step [rank 0, rank 1] as a split of Q, network kind)
+    "raw_vs_two_pass": ((True, False), "chain"),
+    "empty_shard_raw": ((True, True), "chain"),
+    "empty_shard_two_pass": ((False, True), "chain"),
+    "redrawn_binary": ((True, True), "binary"),
+    "redrawn_two_pass": ((True, False), "binary"),
+}
+
+
+def _case_net(kind):
+    from helpers import chain_data, random_dag_data
+
+    if kind == "chain":
+        data, cols, edges = chain_data(6, 4, 3000, 7, stay=0.6)
+        return data, cols, edges, "X5", ["X4", "X2"], 4
+    data, cols, edges = random_dag_data(7, 2, 3, 600, 5)
+    return data, cols, edges, cols[-1], cols[:3], 16
+
+
+STEPS = [(301, 150), (9, 9), (64, 0), (1, 1), (40, 13)]  # (Q, rank-0 rows): uneven, equal, rank 1 empty, ...
+
+
+def _sharded_worker(rank, world, port, case, out_dir):
+    import json
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    from helpers import make_bn, sample_evidence
+    from oracle.ref_infer import OracleBN
+
+    import continuousbayesiannetwork_amd.distributed as D
+    from continuousbayesiannetwork_amd import BayesianNetwork
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    raw_ok, kind = CASES[case]
+    data, cols, edges, target, evk, N = _case_net(kind)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device="cpu")
+    eng = _OracleEngine(bn, OracleBN(edges, cols, data), raw_ok[rank])
+    log = []
+    D.dist = _LogDist(log)
+    fake = type("BN", (), {})()
+    fake.engine = eng
+    try:
+        for k, (Q, q0) in enumerate(STEPS):
+            ev = {c: torch.tensor(v) for c, v in sample_evidence(data, cols, evk, Q, 50 + k).items()}
+            eng._keys = list(ev.keys())
+            lo, hi = (0, q0) if rank == 0 else (q0, Q)
+            mine = {c: v[lo:hi] for c, v in ev.items()}
+            random.seed(1000 + k if rank == 0 else 777)  # only rank 0's draws may matter
+            rows, _ = D.sharded_infer(fake, target, mine, N, gather=True)
+            np.save(os.path.join(out_dir, f"{case}_r{rank}_s{k}.npy"), rows.numpy())
+    finally:
+        D.dist = dist
+    with open(os.path.join(out_dir, f"{case}_log{rank}.json"), "w") as fh:
+        json.dump(log, fh)
+    dist.destroy_process_group()
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_sharded_infer_collectives_two_ranks(tmp_path, case):
+    """sharded_infer on two gloo ranks with the oracle as the device: every
+    rank issues the same collectives in the same order whatever its own plan
+    can do (raw launch on one rank only -> both go two-pass; an empty shard
+    contributes zero max words), redrawn sample domains (binary variables at
+    N_max = 16, node.py:302-333) use rank 0's draws on both ranks, and every
+    rank's gathered rows equal the single-process oracle under rank 0's seed
+    (bayesian_network.py:296: one global max)."""
+    import json
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    from helpers import sample_evidence
+    from oracle.ref_infer import OracleBN
+
+    mp.spawn(_sharded_worker, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
+    data, cols, edges, target, evk, N = _case_net(CASES[case][1])
+    ora = OracleBN(edges, cols, data)
+    for k, (Q, _) in enumerate(STEPS):
+        random.seed(1000 + k)
+        ref, _ = ora.infer(target, sample_evidence(data, cols, evk, Q, 50 + k), N)
+        for r in range(2):
+            np.testing.assert_array_equal(np.load(tmp_path / f"{case}_r{r}_s{k}.npy"), ref)
+    logs = [json.load(open(tmp_path / f"{case}_log{r}.json")) for r in range(2)]
+    assert [e[0] for e in logs[0]] == [e[0] for e in logs[1]]
+    if CASES[case][1] == "binary":
+        assert sum(e[0] == "broadcast_object_list" for e in logs[0]) == len(STEPS)  # one draw exchange per call

@@ -125,3 +125,34 @@ def test_stepper_gather_one_rank(every, gpu):
         if q:
             np.testing.assert_array_equal(o.cpu().numpy(), r.cpu().numpy())
     st.close()
+
+
+def test_stepper_rebinds_after_refit_and_other_networks_keep_plans(gpu):
+    """A refit of one of the network's nodes destroys its plans; the
+    ShardedStepper, which holds the raw plan handle natively, finishes what it
+    enqueued and rebinds to the rebuilt plan (no launch on a freed plan).  A
+    refit in ANOTHER network leaves this network's plans alone."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper
+
+    data, cols, edges = chain_data(8, 4, 4000, 5, stay=0.8)
+    data2, _, _ = chain_data(8, 4, 4000, 6, stay=0.3)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    other = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    ev = _t(sample_evidence(data, cols, ["X6", "X3"], 2000, 3), gpu)
+    st = ShardedStepper(bn, "X7", 4, exchange_every=4)
+    r0, _ = st.step(ev)
+    h0 = next(iter(bn.engine._plans.values())).handle.value
+    ep = bn.engine.epoch
+    other.nodes_obj["X7"].fit(torch.tensor(data2[:, 7], device=gpu), torch.tensor(data2[:, 6][None, :], device=gpu))
+    r1, _ = st.step(ev)  # another network changed: same plan
+    assert bn.engine.epoch == ep and next(iter(bn.engine._plans.values())).handle.value == h0
+    bn.nodes_obj["X7"].fit(torch.tensor(data2[:, 7], device=gpu), torch.tensor(data2[:, 6][None, :], device=gpu))
+    r2, _ = st.step(ev)  # this network changed: plans rebuilt, the stepper rebinds
+    assert bn.engine.epoch == ep + 1
+    st.wait()
+    torch.cuda.synchronize()
+    st.close()
+    a = bn.infer("X7", ev, N_max=4)[0]
+    np.testing.assert_array_equal(r2.cpu().numpy(), a.cpu().numpy())
+    np.testing.assert_array_equal(r0.cpu().numpy(), r1.cpu().numpy())
+    assert not np.array_equal(r1.cpu().numpy(), r2.cpu().numpy())

@@ -593,3 +593,42 @@ def test_redrawn_domains_reuse_one_plan(gpu):
             np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
         kept = [k for k in bn.engine._plans if k[0] == "redrawn"]
         assert len(kept) == 1 and len(bn.engine._plans) == 1
+
+
+def test_redrawn_domains_on_the_sharded_path(gpu):
+    """Binary variables at N_max = 16 (the reference's default, so every
+    sampled domain is padded with random draws per call, node.py:302-333): the
+    one-rank sharded_infer, the engine's prepare() (the two-pass route) and the
+    ShardedStepper serve the redrawn plan, and each call equals infer drawn
+    with the same seed bit for bit (table and direct plans)."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper, sharded_infer
+
+    data, cols, edges = random_dag_data(9, 2, 3, 4000, 13)
+    target = cols[-1]
+    ora = OracleBN(edges, cols, data)
+    ev = sample_evidence(data, cols, cols[:4], 3000, 8)
+    for force_direct in (False, True):
+        bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+        bn.engine.force_direct = force_direct
+        assert bn.engine.redraws(target, ev.keys(), 16)
+        for seed in (5, 6):
+            random.seed(seed)
+            a, adom = bn.infer(target, _t(ev, gpu), N_max=16)
+            a = a.clone()
+            random.seed(seed)
+            ref, _ = ora.infer(target, ev, 16)
+            np.testing.assert_allclose(a.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+            random.seed(seed)
+            b, bdom = sharded_infer(bn, target, _t(ev, gpu), N_max=16)
+            np.testing.assert_array_equal(b.cpu().numpy(), a.cpu().numpy())
+            np.testing.assert_array_equal(bdom.cpu().numpy(), adom.cpu().numpy())
+            random.seed(seed)
+            plan, cols_, nq, _, dev = bn.engine.prepare(target, _t(ev, gpu), 16)
+            assert nq == 3000 and not plan.deterministic
+            st = ShardedStepper(bn, target, 16, exchange_every=2)
+            random.seed(seed)
+            c, _ = st.step(_t(ev, gpu))
+            st.wait()
+            torch.cuda.synchronize()
+            st.close()
+            np.testing.assert_array_equal(c.cpu().numpy(), a.cpu().numpy())

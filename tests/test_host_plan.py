@@ -92,3 +92,62 @@ def test_host_sample_points_match_sample_domain():
         assert torch.equal(a.cpu(), b.cpu())
         dom = nd.info["X2"][3]
         assert torch.equal(domain_index(b, dom).cpu(), domain_index_host(b.cpu(), dom.cpu()))
+
+
+def _redraw_case(edges, cols, data, target, observed, N, seeds):
+    """host_fast.redraw (RedrawProgram jobs, one native call) == the index
+    arrays of build_factor_specs' points under the same seed, same random
+    consumption, same target domain."""
+    from continuousbayesiannetwork_amd import _native
+    from continuousbayesiannetwork_amd.base.node import uniforms
+    from continuousbayesiannetwork_amd.inference.engine import InferenceEngine, Plan, RedrawProgram
+
+    bn = make_bn(BayesianNetwork, edges, cols, data, device="cpu")
+    eng = bn.engine
+    obs = frozenset(observed)
+
+    def walk_plan():
+        order, specs, tdom, det = build_factor_specs(bn, target, obs, N)
+        p = Plan(target, N, order, specs, [], tdom, False, det)
+        InferenceEngine._alloc_index_arrays(p, torch.device("cpu"))
+        for f in range(len(specs)):
+            eng._index_arrays(p, f, bn.nodes_obj[specs[f].node].estimator.domains, 0)
+        return p
+
+    random.seed(1)
+    p = walk_plan()
+    assert not p.deterministic
+    prog = RedrawProgram(bn, p, obs)
+    idx = p.idx_flat.clone()
+    for s in seeds:
+        random.seed(s)
+        want = walk_plan()
+        r_after_walk = random.random()
+        random.seed(s)
+        _native.load_host().redraw(uniforms(prog.total), prog.meta, prog.lospan, prog.doms, idx, prog.pts, N)
+        assert random.random() == r_after_walk
+        assert torch.equal(idx, want.idx_flat)
+        if prog.target_pts:
+            assert torch.equal(prog.pts, want.target_domain.cpu())
+
+
+def test_redraw_program_binary_network():
+    """Binary variables at N_max = 16: every domain padded by 14 draws
+    (node.py:302-333), free and observed parents, the target's own points."""
+    from helpers import random_dag_data
+
+    data, cols, edges = random_dag_data(7, 2, 3, 400, 5)
+    target = cols[-1]
+    _redraw_case(edges, cols, data, target, cols[:2], 16, seeds=(3, 4, 99))
+    _redraw_case(edges, cols, data, target, [], 16, seeds=(7,))
+
+
+def test_redraw_program_mixed_cards():
+    """Mixed domain sizes: some sample_domain calls deterministic (N <=
+    |domain|: no draws, fixed indices), some redrawn."""
+    from helpers import chain_data
+
+    data, cols, edges = chain_data(6, 5, 800, 3, values=[0.0, 0.25, 0.5, 0.75, 1.0])
+    data[:, 2] = np.round(data[:, 2] * 4) % 2  # a binary column among 5-level ones
+    for N in (3, 5, 8):
+        _redraw_case(edges, cols, data, "X5", ["X1", "X3"], N, seeds=(1, 2))
