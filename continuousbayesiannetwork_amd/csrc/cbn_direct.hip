@@ -482,7 +482,12 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
                 if (!h.parent_sample_idx) return set_err(CBN_E_ARG, "factor %d: free parent without samples", f);
                 c.sample_idx = h.parent_sample_idx + (long long)p * N;
                 ++d.n_free;
-                if (F > (1LL << 40) / N) return set_err(CBN_E_LIMIT, "factor %d: too many free-parent combos", f);
+                // each (query, column) thread loops over the F free-parent combos
+                // serially; the reference materialises Q x F x N pdf values for
+                // the same factor (node.py:335-375), so beyond 2^20 combos
+                // neither finishes in useful time
+                if (F > (1LL << 20) / N)
+                    return set_err(CBN_E_LIMIT, "factor %d: more than 2^20 free-parent sample combos", f);
                 F *= N;
             }
         }

@@ -425,18 +425,25 @@ class Stepper {
         const auto t1 = clk::now();
         at::Tensor ret = item.full.defined() ? item.full : item.rows;
         float* rows = static_cast<float*>(item.rows.data_ptr());
+        int launch_rc = 0;
         int rc = ring_.step(
             [&](Slot s) -> int {
                 int* w = ops.slot_words(s);
-                if (n == 0) {  // empty shard: contributes zero words, still joins the group's collectives
-                    CBN_HIP_OK(hipMemsetAsync(w, 0, sizeof(int) * ops.W, ops.A()));
-                    return 0;
+                if (n > 0) {
+                    launch_rc = run_(plan_, n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()),
+                                     reinterpret_cast<unsigned*>(w), rows, flags, ops.A());
+                    if (!launch_rc) return 0;
                 }
-                return run_(plan_, n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()), reinterpret_cast<unsigned*>(w),
-                            rows, flags, ops.A());
+                // empty shard, or a launch the library refused (e.g. the plan's
+                // earlier fused call timed out): zero words, and the step still
+                // joins its group's collectives so every rank's exchanges stay
+                // paired; a refusal is reported after the step is enqueued
+                CBN_HIP_OK(hipMemsetAsync(w, 0, sizeof(int) * ops.W, ops.A()));
+                return 0;
             },
             std::move(item));
         if (rc) return py::int_(rc);
+        if (launch_rc) return py::int_(launch_rc);
         const auto t2 = clk::now();
         tacc_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
         tacc_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();

@@ -17,7 +17,10 @@ high-cardinality columns: the table is prod(cards) while the reference only
 stores the U unique rows), ``fit`` compiles a SPARSE CPD instead: the U
 conditionals keyed by their mixed-radix domain index in an open-addressing
 hash table of 2^ceil(log2 2U) slots (``cbn_hash_build``), evaluated by
-``cbn_cpd_ref_eval`` and by direct inference plans (csrc/cbn_direct.hip).
+``cbn_cpd_ref_eval`` and by direct inference plans (csrc/cbn_direct.hip).  The
+key is an int64, so the product of the column cardinalities must stay below
+2^62 (e.g. four columns of ~60 000 distinct values, or five of ~6 000); a
+larger node raises NotImplementedError when it is first evaluated.
 
 The table is compiled lazily on first device use, so the host logic can be
 exercised without a GPU; every evaluation requires the HIP library.
@@ -33,6 +36,7 @@ from .. import _native
 from ..base.parameter_learning import BaseParameterLearningEstimator
 
 MAX_DENSE_CELLS = 1 << 24  # 64 MiB of fp32 per dense CPD; larger CPDs are hashed
+MAX_KEY_CELLS = 1 << 62  # hashed CPDs: mixed-radix int64 keys over the columns' domain indices
 
 
 def sparse_conditionals(cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool) -> torch.Tensor:
@@ -122,10 +126,17 @@ class BruteForce(BaseParameterLearningEstimator):
         assert self.mle_tensor is not None, "MLE tensor not fitted yet. Call _fit() first."
         if self._compiled:
             return self.cpd
-        dev = _native.require_gpu(self.mle_tensor.device)
-        lib = _native.load()
         cards = self.cards
         n_cells = self.n_cells()
+        if n_cells >= MAX_KEY_CELLS:
+            # the hashed CPD keys a row by its mixed-radix domain index in an
+            # int64 (the direct plans add free-parent terms to a precomputed
+            # partial key): beyond 2^62 cells that index no longer fits
+            raise NotImplementedError(
+                f"BruteForce CPD over {len(cards)} columns with {n_cells:.3e} value combinations (cards {cards}): "
+                f"hashed CPD keys are mixed-radix int64 indices, limited to < 2^62 combinations")
+        dev = _native.require_gpu(self.mle_tensor.device)
+        lib = _native.load()
         with torch.cuda.device(dev):
             rows = self._rows.to(dev)
             probs = self._probs.to(dev)

@@ -156,3 +156,24 @@ def test_stepper_rebinds_after_refit_and_other_networks_keep_plans(gpu):
     np.testing.assert_array_equal(r2.cpu().numpy(), a.cpu().numpy())
     np.testing.assert_array_equal(r0.cpu().numpy(), r1.cpu().numpy())
     assert not np.array_equal(r1.cpu().numpy(), r2.cpu().numpy())
+
+
+def test_variable_elimination_query_matches_reference_golden(gpu):
+    """cbn.inference.VariableElimination.query (the north star's entry point;
+    the reference's ExactInference is a stub, so query is BayesianNetwork.infer,
+    bayesian_network.py:208-305) against a reference-generated golden, through
+    the plugin object the network constructs and through a standalone one."""
+    from continuousbayesiannetwork_amd.inference import INFERENCE_OBJS, VariableElimination
+    from golden_io import load_golden
+
+    g = load_golden("chain5_d4_q1024_parent")
+    m = g["meta"]
+    bn = make_bn(BayesianNetwork, m["edges"], m["columns"], g["data"], device=gpu)
+    ev = _t({k: g["evidence"][k] for k in m["evidence"]}, gpu)
+    assert isinstance(bn.inference_obj, INFERENCE_OBJS["exact"])
+    for ve in (VariableElimination({"inference_obj": "exact"}, bn=bn, device=gpu), bn.inference_obj):
+        random.seed(m["seed"])
+        pdf, dom = (ve.query(m["target"], ev, N_max=m["N_max"]) if hasattr(ve, "query")
+                    else ve.infer(m["target"], ev, None, N_max=m["N_max"]))
+        np.testing.assert_array_equal(dom.cpu().numpy(), g["domain"])
+        np.testing.assert_allclose(pdf.cpu().numpy(), g["pdf"], rtol=RTOL, atol=ATOL)

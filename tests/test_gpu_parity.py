@@ -511,13 +511,14 @@ def test_grid_beyond_64_factors_and_evidence_columns(gpu):
         assert part.shape[0] == 150
 
 
-def test_grid_full_config4_shape_matches_oracle_fixture(gpu):
+def test_grid_full_config4_shape_matches_reference_and_oracle(gpu):
     """The full configs[4] plan (10 x 10 grid, d = N = 64, 100 factors, 99
     evidence columns, 85 MB global-table image) with peaked CPDs whose fp32
-    products stay finite, vs the oracle's marginals committed by
-    tests/golden/make_grid_oracle.py (data + evidence regenerated from the same
-    seeds); the raw launch + scale path (sharded_infer, no process group)
-    == the single call bit for bit."""
+    products stay finite, vs the REFERENCE's own infer on the same 64 queries
+    (tests/golden/make_golden_full.py grid10_d64_peaked_ref64) and the oracle's
+    marginals (tests/golden/make_grid_oracle.py; data + evidence regenerated
+    from the same seeds); the raw launch + scale path (sharded_infer, no
+    process group) == the single call bit for bit."""
     import os
 
     from continuousbayesiannetwork_amd.distributed import sharded_infer
@@ -534,6 +535,10 @@ def test_grid_full_config4_shape_matches_oracle_fixture(gpu):
     out = pdf.cpu().numpy()
     assert np.isfinite(out).all()
     np.testing.assert_allclose(out, z["pdf"], rtol=RTOL, atol=ATOL)
+    zr = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "grid10_d64_peaked_ref64.npz"))
+    assert list(zr["rows"]) == list(range(64))
+    np.testing.assert_array_equal(dom.cpu().numpy()[:1], zr["domain"][:1])
+    np.testing.assert_allclose(out, zr["pdf"], rtol=RTOL, atol=ATOL)
     one, _ = sharded_infer(bn, target, ev, N_max=64)
     np.testing.assert_array_equal(one.cpu().numpy(), out)
 

@@ -85,3 +85,18 @@ def test_oracle_matches_full_batch_golden(name, gen):
     np.testing.assert_array_equal(dom, np.broadcast_to(rdom[:1], dom.shape))
     assert pdf[-1].max() == 1.0
     np.testing.assert_allclose(pdf, ref[pick], rtol=RTOL, atol=ATOL)
+
+
+def test_grid_oracle_fixture_matches_reference_run():
+    """BASELINE configs[4]'s plan (10 x 10 grid, d = N = 64, 100 factors): the
+    oracle fixture (tests/golden/make_grid_oracle.py, 64 queries) against the
+    reference's own infer on the same 64 queries (make_golden_full.py
+    grid10_d64_peaked_ref64), at the north-star tolerance; same domain."""
+    import os
+
+    rows, ref, rdom, m = _full("grid10_d64_peaked_ref64")
+    assert m["Q"] == 64 and list(rows) == list(range(64)) and m["N_max"] == 64
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "grid10_d64_peaked_oracle.npz"))
+    assert (rdom == rdom[:1]).all() and (z["domain"] == rdom[:1]).all()
+    assert np.isfinite(ref).all() and ref.max() == 1.0
+    np.testing.assert_allclose(z["pdf"], ref, rtol=RTOL, atol=ATOL)

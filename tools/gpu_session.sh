@@ -39,6 +39,8 @@ for s in "$@"; do
     param) step pytest_param 400 python -u -m pytest tests/test_gpu_param.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     cont) step bench_cont 400 python tools/bench_cont.py ;;
     alarm) step bench_alarm 400 python tools/bench_alarm.py ;;
+    direct) step bench_direct 400 python tools/bench_direct.py ;;
+    newtests) step pytest_new 400 python -u -m pytest tests/test_gpu_api.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "redrawn or rebinds or stepper" ;;
     grid) step bench_grid 600 python tools/bench_grid.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
