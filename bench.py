@@ -92,6 +92,9 @@ def parse():
                     help="run the N>1 step (raw launch + RCCL all-reduce + scale, pipelined) even at N=1")
     ap.add_argument("--serial-exchange", action="store_true",
                     help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
+    ap.add_argument("--no-fold", action="store_true",
+                    help="N>1 rank-local: a separate batched scale launch per group instead of each step's division "
+                         "folded into a later raw launch (cbn_plan_run_fold)")
     ap.add_argument("--exchange-every", type=int, default=8,
                     help="N>1: steps per all-reduce + scale group (1..8)")
     ap.add_argument("--gather", action="store_true",
@@ -245,13 +248,13 @@ def main():
     # (distributed.ShardedStepper)
     gather = sharded and a.gather
     stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                             force_exchange=sharded, gather=gather)
+                             force_exchange=sharded, gather=gather, fold=not a.no_fold)
 
     def step():
         ev = batches[it[0] % len(batches)]
         it[0] += 1
         if sharded:
-            rows = stepper.step(ev)
+            rows = stepper.step(ev, total_rows=Q * world if stepper.gather else None)
             if a.serial_exchange:
                 stepper.wait()
             return rows
@@ -289,8 +292,9 @@ def main():
     t0 = time.perf_counter()
     ev0.record()  # the library launches on torch's current stream: these events bracket every launch
     for i in range(K):
-        # two-launch path: HIP events recorded inside the library around the passes of every 8th step
-        bn.engine.timed = not sharded and not fused and i % 8 == 7
+        # two-launch path / the sharded step's raw launch: HIP events recorded inside
+        # the library around the launches of every 8th step (on the launch stream)
+        bn.engine.timed = (sharded or not fused) and i % 8 == 7
         step()
     stepper.wait()
     ev1.record()
@@ -307,7 +311,7 @@ def main():
     value = Q * world * K / sec
 
     roofline = None
-    ntimed, tmax_ms, twrite_ms = bn.engine.timing() if not sharded else (0, 0.0, 0.0)
+    ntimed, tmax_ms, twrite_ms = bn.engine.timing()
     bn.engine.check_status()
     if fused:
         # one launch per step: average launch duration = HIP-event time of the timed region / K
@@ -325,6 +329,7 @@ def main():
         # the dominant kernel: fused single launch; beyond its capacity the raw
         # compute pass (then an HBM-bound scale); --two-pass: the write pass
         mode, what, t_dom = ((2, "single launch: both passes", twrite) if fused else
+                             (3, "raw launch of the sharded step", twrite) if sharded else
                              (1, "write pass", twrite) if a.two_pass else (3, "raw compute pass", tmax))
         kname = (f"k_query_staged<{mode}>" if pflags & _native.CBN_PLAN_STAGED
                  else f"k_query_fast<{vpl}, true, {mode}, {nptr}>")  # <MODE> / <VPL, LDS, MODE, NP>
@@ -337,21 +342,22 @@ def main():
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
         roofline["timing"] = ("HIP events on the launch stream around the whole timed region / K launches" if fused
                               else "HIP events around the launches of every 8th step (library-side)")
-        if not fused:
+        if not fused and not sharded:
             roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
-    elif sharded and gather and world > 1:
+    step_info = None
+    if sharded and gather and world > 1:
         # with the reassembly, each rank receives the other ranks' rows every
         # step over xGMI: (world - 1) x Q x 4N bytes -- the dominant transfer
         t_step = ev0.elapsed_time(ev1) / K * 1e-3
         bytes_in = (world - 1) * Q * 4 * d
         achieved = bytes_in / t_step / 1e9
-        roofline = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / XGMI_PEAK_GBS, 4), traffic=None,
-                        kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of the "
-                               "[Q, N] rows (per step)",
-                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_in, timed_steps=K,
-                        timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
-                               "rows received from the other ranks per step")
+        step_info = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
+                         frac=round(achieved / XGMI_PEAK_GBS, 4),
+                         what="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of the "
+                              "[Q, N] rows (per step)",
+                         avg_us=round(t_step * 1e6, 2), bytes_per_step=bytes_in,
+                         timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
+                                "rows received from the other ranks per step")
     elif sharded:
         # sharded step (raw launch + all-reduce(max) of the block words + in-place
         # scale, overlapped across steps): per-GPU algorithmic bytes of one step =
@@ -361,11 +367,11 @@ def main():
         bytes_step = Q * (4 * n_cols + 3 * 4 * d)
         t_step = ev0.elapsed_time(ev1) / K * 1e-3
         achieved = bytes_step / t_step / 1e9
-        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                        kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
-                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_step, timed_steps=K,
-                        timing="HIP events on rank 0's launch stream around the timed region / K steps")
+        step_info = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                         frac=round(achieved / HBM_PEAK_GBS, 4),
+                         what="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
+                         avg_us=round(t_step * 1e6, 2), bytes_per_step=bytes_step,
+                         timing="HIP events on rank 0's launch stream around the timed region / K steps")
 
     other = None
     if sharded:
@@ -374,7 +380,7 @@ def main():
         # (with --gather) each rank keeping its rows (value_rank_local)
         stepper.close()
         stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                                 force_exchange=True, gather=not gather)
+                                 force_exchange=True, gather=not gather, fold=not a.no_fold)
         for _ in range(a.warmup):
             step()
         stepper.wait()
@@ -408,6 +414,7 @@ def main():
                                " + RCCL all-gather of the [Q, N] marginal tensor on every rank" if gather else "")
                            if sharded else "")},
             "roofline": roofline, "cpu_baseline": cpu,
+            **({"sharded_step": step_info} if step_info else {}),
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
             "evidence_batches": len(batches),
         }

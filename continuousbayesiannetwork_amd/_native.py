@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 CBN_MAX_PARENTS = 8
 CBN_MAX_DIRECT_PARENTS = 32
 CBN_MAX_EVIDENCE = 256
@@ -141,6 +141,9 @@ _SIGNATURES = {
     "cbn_scale_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_int32, ctypes.c_void_p]),
     "cbn_plan_max_words": (ctypes.c_int32, [ctypes.c_void_p]),
+    "cbn_plan_run_fold": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "cbn_plan_create_param": (ctypes.c_int, [ctypes.POINTER(ParamFactor), ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_void_p)]),
     "cbn_param_eval": (ctypes.c_int, [ctypes.POINTER(ParamModel), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,

@@ -636,6 +636,64 @@ __device__ __forceinline__ unsigned slot_barrier_max(unsigned* __restrict__ sync
     return wave_max_u(gm);  // non-negative floats: unsigned order == float order
 }
 
+#ifdef CBN_BAR2
+// Diagnostic A/B (tools/ab_libs.sh): two-level form of slot_barrier_max.  The
+// blocks of one group (blockIdx % 8: one XCD under the observed round-robin
+// placement -- speed only, the protocol does not depend on it) reduce their
+// 32 slots; each block of the group publishes the same group word {epoch,
+// group max} once it saw all 32 (idempotent stores), and every block then
+// polls the 8 group words: 40 polled words per wave per round instead of 256.
+__device__ __forceinline__ unsigned slot_barrier_max2(unsigned* __restrict__ sync, unsigned epoch, float bm) {
+    const int lane = threadIdx.x & (kWave - 1);
+    unsigned long long* slots = reinterpret_cast<unsigned long long*>(sync + kSlotWordOff);
+    unsigned long long* gslots = slots + kMaxSlots - 8;  // 8 group words: the last slots (fused grid <= #CUs)
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    if (lane == 0)
+        __hip_atomic_store(&slots[blockIdx.x], tag | __float_as_uint(bm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int G = gridDim.x;
+    const int grp = blockIdx.x & 7;
+    unsigned spins = 0;
+    auto timeout = [&]() {
+        if (lane == 0) {
+            atomicOr(&sync[2], 1u);
+            unsigned* hs = *reinterpret_cast<unsigned* const*>(sync + kHostStatusWordOff);
+            if (hs) __hip_atomic_store(hs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    };
+    // level 1: this group's slots grp, grp + 8, ... (< G); lane i owns slot grp + 8 i
+    unsigned gm = 0;
+    for (;;) {
+        const int s = grp + 8 * lane;
+        unsigned long long v = s < G ? __hip_atomic_load(&slots[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
+        const bool here = (v >> 32) == (unsigned long long)epoch;
+        if (__builtin_amdgcn_ballot_w64(!here) == 0) {
+            gm = wave_max_u(s < G ? (unsigned)v : 0u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kSpinLimit) {
+            timeout();
+            return 0x7fc00000u;
+        }
+    }
+    if (lane == 0)
+        __hip_atomic_store(&gslots[grp], tag | gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // level 2: the 8 group words (groups with no block: G < 8)
+    for (;;) {
+        unsigned long long v = (lane < 8 && lane < G) ? __hip_atomic_load(&gslots[lane], __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT) : tag;
+        const bool here = (v >> 32) == (unsigned long long)epoch;
+        if (__builtin_amdgcn_ballot_w64(!here) == 0) return wave_max_u((lane < 8 && lane < G) ? (unsigned)v : 0u);
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kSpinLimit) {
+            timeout();
+            return 0x7fc00000u;
+        }
+    }
+}
+#define slot_barrier_max slot_barrier_max2
+#endif
+
 template <int VPL, bool USE_LDS, int MODE, int NP>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrsT<NP> fp,
@@ -982,11 +1040,30 @@ constexpr int kDmaW = CBN_DMA_WAVES;                 // round 0: waves issuing t
 constexpr int kEvW = kQueryThreads / kWave - kDmaW;  // round 0: waves staging the evidence
 constexpr int kSUp = (64 + kEvW - 1) / kEvW;         // round 0: units per evidence wave
 
+// A raw launch of the pipelined sharded stepper also finishes an EARLIER step:
+// it divides that step's unnormalised rows (n4 float4, this block's slice of
+// `chunk` float4) by the max of its all-reduced words -- the in-place scale of
+// bayesian_network.py:296 -- with the same correctly rounded quotient as
+// k_scale, so a step's rows are bit for bit those of the separate scale.  The
+// loads are issued after the prologue barrier and land during the products;
+// the divided rows are stored before this launch's own rows.  rows == nullptr:
+// nothing to fold.
+struct FoldJob {
+    float* rows;
+    const unsigned* words;
+    long long n4;
+    long long chunk;
+    int n_words;
+};
+constexpr int kFoldK = 2;   // float4 per thread held across the products (chunk <= 2048: one 65 536 x 32 step)
+constexpr int kFoldW = 4;   // words per lane (<= 256 words)
+
 template <int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, int nf, int zero_off, long long Q,
                long long per, unsigned* __restrict__ sync, unsigned epoch, const unsigned* __restrict__ max_in,
-               int n_max, unsigned* __restrict__ max_out, float* __restrict__ out, FPtrsT<kFastPtrsSmall> fp) {
+               int n_max, unsigned* __restrict__ max_out, float* __restrict__ out, FoldJob fold,
+               FPtrsT<kFastPtrsSmall> fp) {
     CBN_STAMP_INIT;
     constexpr int N = 32;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
@@ -1151,6 +1228,25 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     CBN_STAMP(2);
     __syncthreads();  // image landed (vmcnt(0) of the DMA) + round 0 offsets
     CBN_STAMP(3);
+    // raw launch folding an earlier step's scale: its rows and words in flight
+    // during the products (issued here, after the barrier's vmcnt(0))
+    float4 fv[kFoldK];
+    unsigned fw[kFoldW];
+    const long long fb = (long long)blockIdx.x * fold.chunk;
+    const long long fe = fb + fold.chunk < fold.n4 ? fb + fold.chunk : fold.n4;
+    if (MODE == kModeRaw && fold.rows) {  // kernel-uniform
+        const float4* r4 = reinterpret_cast<const float4*>(fold.rows);
+#pragma unroll
+        for (int k = 0; k < kFoldK; ++k) {
+            const long long i = fb + tid + k * kQueryThreads;
+            fv[k] = i < fe ? r4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < kFoldW; ++k) {
+            const int w = lane + k * kWave;
+            fw[k] = w < fold.n_words ? fold.words[w] : 0u;
+        }
+    }
 
     const int qi = lane >> 2;  // query slot in the wave (16 per wave)
     const int l = lane & 3;
@@ -1263,6 +1359,27 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         }
     }
     CBN_STAMP(6);
+    if (MODE == kModeRaw && fold.rows) {  // kernel-uniform: the earlier step's slice, divided and stored
+        unsigned m = 0;
+#pragma unroll
+        for (int k = 0; k < kFoldW; ++k) m = max(m, fw[k]);
+        m = wave_max_u(m);
+        const double y = 1.0 / (double)__uint_as_float(m);  // acc / max correctly rounded (see the fused epilogue)
+        float4* r4 = reinterpret_cast<float4*>(fold.rows);
+#pragma unroll
+        for (int k = 0; k < kFoldK; ++k) {
+            const long long i = fb + tid + k * kQueryThreads;
+            if (i < fe)
+                r4[i] = make_float4((float)((double)fv[k].x * y), (float)((double)fv[k].y * y),
+                                    (float)((double)fv[k].z * y), (float)((double)fv[k].w * y));
+        }
+        // a slice beyond kFoldK float4 per thread (batches larger than the launch's grid x 2048)
+        for (long long i = fb + tid + kFoldK * kQueryThreads; i < fe; i += kQueryThreads) {
+            const float4 v = r4[i];
+            r4[i] = make_float4((float)((double)v.x * y), (float)((double)v.y * y), (float)((double)v.z * y),
+                                (float)((double)v.w * y));
+        }
+    }
     if (MODE == kModeMax || MODE == kModeRaw) {
         lmax = wave_max(lmax);
         if (lane == 0) wmax[wid] = lmax;
@@ -1342,6 +1459,10 @@ __global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long lon
 // pair b, dividing by the max of max_in[b * n_max, (b + 1) * n_max)): the
 // pipelined sharded stepper exchanges and scales several steps at once.
 constexpr int kScaleBatch = 8;
+#ifndef CBN_SCALE_U
+#define CBN_SCALE_U 8
+#endif
+constexpr int kScaleU = CBN_SCALE_U;
 struct ScaleBatch {
     float* out[kScaleBatch];
     long long n[kScaleBatch];
@@ -1359,7 +1480,26 @@ __global__ void __launch_bounds__(256) k_scale_batch(ScaleBatch sb, const unsign
     const long long n4 = n / 4;
     float4* o4 = reinterpret_cast<float4*>(out);
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    // kScaleU float4 per thread in flight: a small grid (it runs beside the
+    // next steps' raw launches on the comm stream, in the wave slots those
+    // leave free) still streams at HBM rate
+    constexpr int U = kScaleU;
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = o4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u].x = v[u].x / m;
+            v[u].y = v[u].y / m;
+            v[u].z = v[u].z / m;
+            v[u].w = v[u].w / m;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) o4[i + u * stride] = v[u];
+    }
+    for (; i < n4; i += stride) {
         float4 v = o4[i];
         v.x = v.x / m;
         v.y = v.y / m;
@@ -1367,8 +1507,8 @@ __global__ void __launch_bounds__(256) k_scale_batch(ScaleBatch sb, const unsign
         v.w = v.w / m;
         o4[i] = v;
     }
-    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
-        out[i] = out[i] / m;
+    for (long long j = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += stride)
+        out[j] = out[j] / m;
 }
 
 // *out = max of n words (public query_max: per-block maxima -> one word)
@@ -1437,13 +1577,20 @@ void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvP
 
 template <int VPL, bool LDS, int MODE>
 void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
-                   unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out) {
+                   unsigned epoch, const unsigned* max_in, int n_max, unsigned* max_out, float* out,
+                   const FoldJob* fold = nullptr) {
     if (p->staged) {  // paired N = 32 layout in LDS: the staged kernel (same grid, same words)
+        FoldJob fj;
+        memset(&fj, 0, sizeof(fj));
+        if (fold && fold->rows && fold->n4 > 0) {
+            fj = *fold;
+            fj.chunk = (fj.n4 + blocks - 1) / blocks;
+        }
         // factors [prefix, nf): the prefix is folded into factor `prefix`'s table
         hipLaunchKernelGGL((k_query_staged<MODE>), dim3(blocks), dim3(kQueryThreads), p->staged_lds_bytes, s,
                            p->d_image, p->image_floats, p->rec_off + p->prefix * kRecFloats, p->nf - p->prefix,
                            p->zero_off, Q, (Q + blocks - 1) / blocks, p->d_sync, epoch, max_in, n_max, max_out, out,
-                           fast_ptrs<kFastPtrsSmall>(p, ev, p->prefix));
+                           fj, fast_ptrs<kFastPtrsSmall>(p, ev, p->prefix));
         return;
     }
     if (p->nf * kFastObs <= kFastPtrsSmall)
@@ -1497,12 +1644,14 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
 }
 
 template <int VPL, bool LDS>
-int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
+int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s,
+                 const FoldJob* fold = nullptr) {
     const int L = p->N / (4 * VPL);
     const long long cap = p->max_slots;
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
-    launch_fast_k<VPL, LDS, kModeRaw>(p, (unsigned)blocks, s, ev, Q, L, 0u, nullptr, p->max_slots, max_bits, out);
+    launch_fast_k<VPL, LDS, kModeRaw>(p, (unsigned)blocks, s, ev, Q, L, 0u, nullptr, p->max_slots, max_bits, out,
+                                      fold);
     HIP_TRY(hipGetLastError());
     return CBN_OK;
 }
@@ -2202,6 +2351,60 @@ int cbn_plan_run(cbn_plan* plan, int64_t n_queries, const float* const* evidence
     return CBN_OK;
 }
 
+int cbn_plan_run_fold(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+                      uint32_t* max_bits, float* out, float* fold_rows, int64_t fold_n_elems,
+                      const uint32_t* fold_words, int32_t fold_n_words, int32_t flags, void* stream) {
+    if (!plan) return set_err(CBN_E_ARG, "null plan");
+    if (!fold_rows || fold_n_elems <= 0) return cbn_plan_run(plan, n_queries, evidence, n_evidence, max_bits, out,
+                                                             flags | CBN_RUN_RAW, stream);
+    if (!plan->fast || !plan->staged || plan->direct || plan->param)
+        return set_err(CBN_E_UNSUPPORTED, "cbn_plan_run_fold: needs a staged (paired N = 32) table plan");
+    if (fold_n_elems % 4 || reinterpret_cast<uintptr_t>(fold_rows) % 16 || !fold_words || fold_n_words < 1 ||
+        fold_n_words > kFoldW * kWave)
+        return set_err(CBN_E_ARG, "cbn_plan_run_fold: fold rows must be 16-B aligned float4s, 1..%d words",
+                       kFoldW * kWave);
+    if (plan->h_status && __atomic_load_n(plan->h_status, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(plan->h_status, 0u, __ATOMIC_RELEASE);
+        return set_err(CBN_E_TIMEOUT, "an earlier single-launch call of this plan timed out in its grid barrier "
+                                      "(not every block was resident); its rows are NaN");
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if (flags & CBN_RUN_BUILD_TABLES) {
+        rc = cbn_plan_build_tables(plan, stream);
+        if (rc) return rc;
+    }
+    if (n_evidence != plan->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", plan->ns, n_evidence);
+    if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run_fold: null output");
+    if (n_queries <= 0) return set_err(CBN_E_ARG, "cbn_plan_run_fold: raw launch needs >= 1 query");
+    EvPtrs ev;
+    memset(&ev, 0, sizeof(ev));
+    for (int i = 0; i < n_evidence; ++i) {
+        if (!evidence[i]) return set_err(CBN_E_ARG, "null evidence column %d", i);
+        ev.p[i] = evidence[i];
+    }
+    hipEvent_t* e = nullptr;
+    if ((flags & CBN_RUN_TIMED) && plan->ev_n < cbn_plan::kRing) {
+        e = plan->ev[plan->ev_n];
+        for (int k = 0; k < 3; ++k)
+            if (!e[k]) HIP_TRY(hipEventCreate(&e[k]));
+        ++plan->ev_n;
+        HIP_TRY(hipEventRecord(e[0], s));
+        HIP_TRY(hipEventRecord(e[1], s));
+    }
+    FoldJob fj;
+    memset(&fj, 0, sizeof(fj));
+    fj.rows = fold_rows;
+    fj.words = fold_words;
+    fj.n4 = fold_n_elems / 4;
+    fj.n_words = fold_n_words;
+    rc = plan->vpl == 2 ? launch_raw_v<2, true>(plan, n_queries, ev, max_bits, out, s, &fj)
+                        : launch_raw_v<1, true>(plan, n_queries, ev, max_bits, out, s, &fj);
+    if (rc) return rc;
+    if (e) HIP_TRY(hipEventRecord(e[2], s));
+    return CBN_OK;
+}
+
 int cbn_plan_status(cbn_plan* plan, int32_t* status) {
     if (!plan || !status) return set_err(CBN_E_ARG, "cbn_plan_status: bad arguments");
     unsigned v = 0;
@@ -2234,6 +2437,18 @@ int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, vo
     return launch_scale(out, (long long)n, max_bits, (int)n_max, nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
+namespace {
+// blocks per CU of the batched scale (CBN_SCALE_BLOCKS_PER_CU, A/B knob)
+int scale_blocks_per_cu() {
+    static int v = [] {
+        const char* e = getenv("CBN_SCALE_BLOCKS_PER_CU");
+        const int x = e ? atoi(e) : 0;
+        return x >= 1 && x <= 16 ? x : 1;
+    }();
+    return v;
+}
+}  // namespace
+
 int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batches, const uint32_t* max_bits,
                     int32_t n_max, void* stream) {
     if (n_batches < 0 || n_batches > kScaleBatch || n_max < 1 || (n_batches > 0 && (!outs || !n_elems || !max_bits)))
@@ -2249,8 +2464,10 @@ int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batche
         sb.n[b] = n_elems[b];
         most = std::max(most, (long long)n_elems[b]);
     }
-    long long blocks = (most / 4 + 255) / 256;
-    const long long cap = std::max(1LL, 4LL * num_cu() / n_batches);
+    // grid: scale_blocks_per_cu() 256-thread blocks per CU over all batches (each
+    // thread kScaleU float4 in flight)
+    long long blocks = (most / 4 + 256LL * kScaleU - 1) / (256LL * kScaleU);
+    const long long cap = std::max(1LL, (long long)scale_blocks_per_cu() * num_cu() / n_batches);
     blocks = std::max(1LL, std::min(blocks, cap));
     hipLaunchKernelGGL(k_scale_batch, dim3((unsigned)blocks, (unsigned)n_batches), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), sb, max_bits, (int)n_max);

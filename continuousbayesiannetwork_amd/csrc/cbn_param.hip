@@ -336,7 +336,10 @@ __device__ __forceinline__ float mlp1p(const float* __restrict__ PW, int H, cons
     return mu + PW[0];
 }
 
-template <int ACT>
+// NMAX: the most inputs a factor of the launch can have (the column-table
+// kernels take <= kTabIn): input counts beyond it are not instantiated, so
+// their weight registers do not weigh on the kernel's SGPR allocation
+template <int ACT, int NMAX>
 __device__ __forceinline__ float mlp1p_nin(const float* __restrict__ PW, int n_in, int H, const float (&z)[kMaxP],
                                            int act) {
     switch (n_in) {  // wave-uniform
@@ -344,10 +347,10 @@ __device__ __forceinline__ float mlp1p_nin(const float* __restrict__ PW, int n_i
         case 2: return mlp1p<ACT, 2>(PW, H, z, act);
         case 3: return mlp1p<ACT, 3>(PW, H, z, act);
         case 4: return mlp1p<ACT, 4>(PW, H, z, act);
-        case 5: return mlp1p<ACT, 5>(PW, H, z, act);
-        case 6: return mlp1p<ACT, 6>(PW, H, z, act);
-        case 7: return mlp1p<ACT, 7>(PW, H, z, act);
-        default: return mlp1p<ACT, 8>(PW, H, z, act);
+        case 5: if (NMAX >= 5) return mlp1p<ACT, 5 <= NMAX ? 5 : 1>(PW, H, z, act); [[fallthrough]];
+        case 6: if (NMAX >= 6) return mlp1p<ACT, 6 <= NMAX ? 6 : 1>(PW, H, z, act); [[fallthrough]];
+        case 7: if (NMAX >= 7) return mlp1p<ACT, 7 <= NMAX ? 7 : 1>(PW, H, z, act); [[fallthrough]];
+        default: return mlp1p<ACT, NMAX>(PW, H, z, act);
     }
 }
 
@@ -371,18 +374,19 @@ __device__ __forceinline__ float mlp1p_rt(const float* __restrict__ PW, int n_in
     return mu + PW[0];
 }
 
+template <int NMAX>
 __device__ __forceinline__ float mlp1_packed(const PRec& r, const float* __restrict__ img, const float (&z)[kMaxP]) {
     const float* PW = img + r.pw_off;
     switch (r.m.act) {
-        case CBN_ACT_TANH: return mlp1p_nin<CBN_ACT_TANH>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_TANH);
-        case CBN_ACT_RELU: return mlp1p_nin<CBN_ACT_RELU>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_RELU);
+        case CBN_ACT_TANH: return mlp1p_nin<CBN_ACT_TANH, NMAX>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_TANH);
+        case CBN_ACT_RELU: return mlp1p_nin<CBN_ACT_RELU, NMAX>(PW, r.m.width[0], r.m.width[1], z, CBN_ACT_RELU);
         default: return mlp1p_rt(PW, r.m.width[0], r.m.width[1], z, r.m.act);
     }
 }
 
 // mu of a query factor: HMAX 1 plans hold linear and one-hidden-layer models
 // (the latter always pair-packed)
-template <int HMAX>
+template <int HMAX, int NMAX = kMaxP>
 __device__ __forceinline__ float query_mu(const PRec& r, const float* __restrict__ img, const float* __restrict__ W,
                                           const float (&z)[kMaxP], float* deep);
 
@@ -458,11 +462,11 @@ __device__ __forceinline__ float model_mu(const MDesc& m, const float* __restric
     }
 }
 
-template <int HMAX>
+template <int HMAX, int NMAX>
 __device__ __forceinline__ float query_mu(const PRec& r, const float* __restrict__ img, const float* __restrict__ W,
                                           const float (&z)[kMaxP], float* deep) {
     if (HMAX == 0) return model_mu<0>(r.m, W, z, deep);
-    if (HMAX == 1) return r.m.n_layers == 2 ? mlp1_packed(r, img, z) : model_mu<0>(r.m, W, z, deep);
+    if (HMAX == 1) return r.m.n_layers == 2 ? mlp1_packed<NMAX>(r, img, z) : model_mu<0>(r.m, W, z, deep);
     return model_mu<HMAX, 512>(r.m, W, z, deep);
 }
 
@@ -637,6 +641,7 @@ __global__ void __launch_bounds__(kQThreads)
 k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
               int n_words, unsigned* __restrict__ max_out, float* __restrict__ out, FSplit sp) {
     const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);
+    constexpr int kNMax = TAB ? kTabIn : kMaxP;  // inputs per factor (column-table plans: <= kTabIn)
     // dynamic LDS: [nf x kMaxP InCol] [deep-model scratch, models with >= 2 hidden layers]
     extern __shared__ __attribute__((aligned(16))) float4 smem_q[];
     InCol* incol = reinterpret_cast<InCol*>(smem_q);
@@ -695,7 +700,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 const int mode = mode_of(r.family, r.unit != 0);
                 const float sc = r.scale, isc = r.inv_scale, nm = r.norm;
                 if (r.M == 1) {  // every parent observed: x = pdf (a mean over size-1 axes)
-                    mul_row<NC, MODE>(mode, acc, S, sc, isc, nm, query_mu<HMAX>(r, img, W, z, deep));
+                    mul_row<NC, MODE>(mode, acc, S, sc, isc, nm, query_mu<HMAX, kNMax>(r, img, W, z, deep));
                 } else {
                     float fx[NC], cx[NC];
 #pragma unroll
@@ -712,7 +717,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                                 cc = qd;
                             }
                         }
-                        add_row<NC, MODE>(mode, fx, cx, S, sc, isc, nm, query_mu<HMAX>(r, img, W, z, deep));
+                        add_row<NC, MODE>(mode, fx, cx, S, sc, isc, nm, query_mu<HMAX, kNMax>(r, img, W, z, deep));
                     }
                     const float Mf = (float)r.M;
 #pragma unroll

@@ -28,6 +28,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -546,6 +547,364 @@ int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max)
                                           reinterpret_cast<const unsigned*>(max_ptr), n_max, s);
 }
 
+// ------------------------------------------------- folded-scale stepper ring --
+// The rank-local sharded step without a scale launch: every raw launch also
+// divides ONE earlier step's rows by that step's all-reduced max
+// (cbn_plan_run_fold), so the scale's HBM traffic overlaps the launch's LDS-
+// bound products instead of competing with the next launches for the CUs.
+//   compute stream A: raw launch of step s (words -> set g % kSets, slot i),
+//                     folding the oldest unfinished step of a group exchanged
+//                     two groups back (its all-reduce had a whole group of
+//                     launches to complete)
+//   comm stream C:    after each group's last launch, ONE all-reduce(MAX) of
+//                     the group's words in place
+// Word sets form a ring of kSets groups.  Before a group writes set s, any
+// step whose words are still in s and not yet folded (a group with empty
+// shards or a partial group flushed by wait()) is scaled on A first, and A
+// waits for C's last use of s.  wait() exchanges the partial group and scales
+// every unfinished step on C, then joins.  FoldRing is that bookkeeping only;
+// FoldHipOps binds it to HIP / RCCL / cbn_plan_run_fold, PyFoldOps to Python
+// callbacks (the world-size-2 gloo test drives the same ring on CPU).
+constexpr int kSets = 3;
+
+template <class Item>
+struct FoldPending {
+    Item item;
+    int set;
+    int index;
+};
+
+template <class Ops>
+class FoldRing {
+  public:
+    using Item = typename Ops::Item;
+    using Pending = FoldPending<Item>;
+    FoldRing(Ops ops, int group) : ops_(std::move(ops)), G_(group < 1 ? 1 : (group > 8 ? 8 : group)) {}
+
+    // launch(slot, fold, consumed) writes the step's rows and words slot and,
+    // when `fold` is non-null and the step launches a kernel, finishes that
+    // earlier step (consumed = true).  Returns 0 or a C ABI error code.
+    template <class Launch>
+    int step(Launch&& launch, Item item) {
+        if (cur_.empty()) begin_group();
+        const int set = (int)(g_ % kSets);
+        const Slot slot{set, (int)cur_.size()};
+        const Pending* f = foldq_.empty() ? nullptr : &foldq_.front();
+        bool consumed = false;
+        const int rc = launch(slot, f, consumed);
+        if (rc) return rc;
+        if (consumed) {
+            ops_.folded(foldq_.front());
+            foldq_.pop_front();
+        }
+        cur_.push_back(Pending{std::move(item), set, slot.index});
+        ++k_;
+        if ((int)cur_.size() == G_) return exchange_group();
+        return 0;
+    }
+    // every enqueued step final before the caller's later work on A
+    int wait() {
+        int rc = exchange_group();
+        if (rc) return rc;
+        for (auto& grp : exch_)
+            for (auto& p : grp.items) foldq_.push_back(std::move(p));
+        exch_.clear();
+        rc = scale_runs(foldq_, /*on_comm=*/true);
+        foldq_.clear();
+        if (!rc && k_) ops_.join();
+        return rc;
+    }
+    Ops& ops() { return ops_; }
+    int64_t steps() const { return k_; }
+    int group() const { return G_; }
+    int pending() const { return (int)cur_.size(); }
+    int unfinished() const {
+        size_t n = foldq_.size() + cur_.size();
+        for (auto& g : exch_) n += g.items.size();
+        return (int)n;
+    }
+
+  private:
+    struct Group {
+        int64_t g;
+        std::vector<Pending> items;
+    };
+    void begin_group() {
+        const int set = (int)(g_ % kSets);
+        // steps whose words still sit in `set`: finish them before this group overwrites it
+        std::deque<Pending> here, keep;
+        for (auto& p : foldq_) (p.set == set ? here : keep).push_back(std::move(p));
+        foldq_.swap(keep);
+        for (auto it = exch_.begin(); it != exch_.end();) {
+            if (!it->items.empty() && it->items.front().set == set) {
+                for (auto& p : it->items) here.push_back(std::move(p));
+                it = exch_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        ops_.wait_set(set);  // A after C's last use of the set (its exchange / a wait() scale)
+        if (!here.empty()) scale_runs(here, /*on_comm=*/false);
+        // groups exchanged two or more groups back become foldable
+        while (!exch_.empty() && exch_.front().g <= g_ - 2) {
+            Group& grp = exch_.front();
+            if (!grp.items.empty()) ops_.wait_set(grp.items.front().set);  // their all-reduce done
+            for (auto& p : grp.items) foldq_.push_back(std::move(p));
+            exch_.pop_front();
+        }
+    }
+    int exchange_group() {
+        if (cur_.empty()) return 0;
+        const int set = (int)(g_ % kSets);
+        ops_.handoff();  // C after every launch so far (the group's raw launches and their folds)
+        const int rc = ops_.exchange(set, (int)cur_.size());
+        if (rc) return rc;
+        ops_.mark_set(set, /*on_comm=*/true);
+        exch_.push_back(Group{g_, std::move(cur_)});
+        cur_.clear();
+        ++g_;
+        return 0;
+    }
+    // scale the given steps (runs of consecutive slots of one set per call)
+    int scale_runs(std::deque<Pending>& q, bool on_comm) {
+        size_t i = 0;
+        while (i < q.size()) {
+            size_t j = i + 1;
+            while (j < q.size() && j - i < 8 && q[j].set == q[i].set && q[j].index == q[j - 1].index + 1) ++j;
+            std::vector<const Pending*> run;
+            for (size_t k = i; k < j; ++k) run.push_back(&q[k]);
+            const int rc = ops_.scale(run, on_comm);
+            if (rc) return rc;
+            ops_.mark_set(q[i].set, on_comm);
+            i = j;
+        }
+        return 0;
+    }
+
+    Ops ops_;
+    int G_;
+    std::vector<Pending> cur_;
+    std::deque<Group> exch_;
+    std::deque<Pending> foldq_;
+    int64_t k_ = 0, g_ = 0;
+};
+
+struct FoldItem {
+    at::Tensor rows;  // this rank's [q_r, N] rows (unnormalised until folded / scaled)
+};
+
+// ---- GPU: HIP streams / events, RCCL, cbn_plan_run_fold / cbn_scale_batch
+struct FoldHipOps {
+    using Item = FoldItem;
+    using P = FoldPending<FoldItem>;
+    scale_batch_fn scale_batch = nullptr;
+    ncclComm_t comm = nullptr;
+    int64_t dev = 0, W = 0;
+    int G = 1;
+    c10::hip::HIPStream cs;
+    at::Tensor words;  // [kSets * G, W] int32 on the device
+    hipEvent_t ready = nullptr, tail = nullptr;
+    hipEvent_t set_ev[kSets] = {};
+    bool set_used[kSets] = {};
+
+    FoldHipOps(scale_batch_fn sb, ncclComm_t c, int64_t dev_, int64_t W_, int G_)
+        : scale_batch(sb), comm(c), dev(dev_), W(W_), G(G_),
+          cs(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)dev_)) {
+        words = at::zeros({kSets * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
+        CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));
+        for (auto& e : set_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    FoldHipOps(FoldHipOps&& o) noexcept
+        : scale_batch(o.scale_batch), comm(o.comm), dev(o.dev), W(o.W), G(o.G), cs(o.cs), words(std::move(o.words)),
+          ready(o.ready), tail(o.tail) {
+        for (int s = 0; s < kSets; ++s) {
+            set_ev[s] = o.set_ev[s];
+            set_used[s] = o.set_used[s];
+            o.set_ev[s] = nullptr;
+        }
+        o.ready = o.tail = nullptr;
+    }
+    ~FoldHipOps() {
+        if (ready) (void)hipEventDestroy(ready);
+        if (tail) (void)hipEventDestroy(tail);
+        for (auto e : set_ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    hipStream_t A() const { return c10::hip::getCurrentHIPStream(dev).stream(); }
+    int* slot_words(int set, int index) { return words.data_ptr<int>() + ((int64_t)set * G + index) * W; }
+
+    void wait_set(int set) {
+        if (set_used[set]) CBN_HIP_OK(hipStreamWaitEvent(A(), set_ev[set], 0));
+    }
+    void mark_set(int set, bool on_comm) {
+        CBN_HIP_OK(hipEventRecord(set_ev[set], on_comm ? cs.stream() : A()));
+        set_used[set] = true;
+    }
+    void handoff() {
+        CBN_HIP_OK(hipEventRecord(ready, A()));
+        CBN_HIP_OK(hipStreamWaitEvent(cs.stream(), ready, 0));
+    }
+    int exchange(int set, int nb) {
+        if (comm) {
+            int* w = slot_words(set, 0);
+            CBN_NCCL_OK(g_rccl.all_reduce(w, w, (size_t)nb * W, ncclInt32, ncclMax, comm, cs.stream()));
+        }
+        return 0;
+    }
+    int scale(const std::vector<const P*>& run, bool on_comm) {
+        float* outs[8];
+        int64_t ns[8];
+        const int nb = (int)run.size();
+        for (int b = 0; b < nb; ++b) {
+            outs[b] = static_cast<float*>(run[b]->item.rows.data_ptr());
+            ns[b] = run[b]->item.rows.numel();
+            if (on_comm)  // rows used on C: the caching allocator must not recycle them early
+                c10::hip::HIPCachingAllocator::recordStream(run[b]->item.rows.storage().data_ptr(), cs);
+        }
+        return scale_batch(outs, ns, nb, reinterpret_cast<const unsigned*>(slot_words(run[0]->set, run[0]->index)),
+                           (int32_t)W, on_comm ? cs.stream() : A());
+    }
+    void folded(const P&) {}
+    void join() {
+        CBN_HIP_OK(hipEventRecord(tail, cs.stream()));
+        CBN_HIP_OK(hipStreamWaitEvent(A(), tail, 0));
+    }
+};
+
+using fold_fn = int (*)(void*, int64_t, const float* const*, int32_t, unsigned*, float*, float*, int64_t,
+                        const unsigned*, int32_t, int32_t, hipStream_t);
+
+// distributed.ShardedStepper's rank-local step with folded scales (no gather)
+class FoldStepper {
+  public:
+    FoldStepper(uintptr_t fold_addr, uintptr_t scale_batch_addr, uintptr_t plan, py::tuple slots, py::object first,
+                int64_t device_index, int64_t n_samples, bool target_observed, int64_t n_words, int group,
+                uintptr_t comm)
+        : fold_(reinterpret_cast<fold_fn>(fold_addr)), plan_(reinterpret_cast<void*>(plan)), slots_(slots),
+          first_(first), dev_(device_index), n_samples_(n_samples), target_observed_(target_observed),
+          ring_(FoldHipOps(reinterpret_cast<scale_batch_fn>(scale_batch_addr), reinterpret_cast<ncclComm_t>(comm),
+                           device_index, n_words, group < 1 ? 1 : (group > 8 ? 8 : group)),
+                group) {}
+
+    // this step's rows (final after wait()); None when a fast check failed (the
+    // caller converts the evidence and retries); an int: the C ABI's error code
+    py::object step(py::dict evidence, py::object out_obj, int32_t flags) {
+        Cols c;
+        int64_t n = 0;
+        if (!gather_cols(evidence, c, n)) return py::none();
+        FoldHipOps& ops = ring_.ops();
+        FoldItem item{check_out(out_obj, n, n_samples_, dev_)};
+        at::Tensor ret = item.rows;
+        float* rows = static_cast<float*>(item.rows.data_ptr());
+        int launch_rc = 0;
+        const int rc = ring_.step(
+            [&](Slot s, const FoldPending<FoldItem>* f, bool& consumed) -> int {
+                int* w = ops.slot_words(s.half, s.index);
+                if (n > 0) {
+                    float* fr = f ? static_cast<float*>(f->item.rows.data_ptr()) : nullptr;
+                    const int64_t fn = f ? f->item.rows.numel() : 0;
+                    launch_rc = fold_(plan_, n, c.p, (int32_t)PyTuple_GET_SIZE(slots_.ptr()),
+                                      reinterpret_cast<unsigned*>(w), rows, fn > 0 ? fr : nullptr, fn,
+                                      f ? reinterpret_cast<const unsigned*>(ops.slot_words(f->set, f->index))
+                                        : nullptr,
+                                      (int32_t)ops.W, flags, ops.A());
+                    if (!launch_rc) {
+                        consumed = f != nullptr;
+                        return 0;
+                    }
+                }
+                // empty shard, or a launch the library refused: zero words; the
+                // step still joins its group's all-reduce (paired collectives)
+                CBN_HIP_OK(hipMemsetAsync(w, 0, sizeof(int) * ops.W, ops.A()));
+                return 0;
+            },
+            std::move(item));
+        if (rc) return py::int_(rc);
+        if (launch_rc) return py::int_(launch_rc);
+        return py::cast(ret);
+    }
+    void wait() { check_(ring_.wait()); }
+    void synchronize() {
+        check_(ring_.wait());
+        CBN_HIP_OK(hipStreamSynchronize(ring_.ops().A()));
+    }
+    int64_t steps() const { return ring_.steps(); }
+    int group() const { return ring_.group(); }
+    int unfinished() const { return ring_.unfinished(); }
+
+  private:
+    bool gather_cols(py::dict& evidence, Cols& c, int64_t& n) {
+        if (!first_.is_none()) {
+            PyObject* f = PyDict_GetItem(evidence.ptr(), first_.ptr());
+            if (f && THPVariable_Check(f)) {
+                const at::Tensor& t = THPVariable_Unpack(f);
+                if (t.dim() >= 1 && t.size(0) == 0) {
+                    n = 0;
+                    return true;
+                }
+            }
+        }
+        if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return false;
+        n = c.n;
+        return true;
+    }
+    static void check_(int rc) {
+        if (rc) throw std::runtime_error("cbn_scale_batch failed (rc=" + std::to_string(rc) + ")");
+    }
+    fold_fn fold_;
+    void* plan_;
+    py::tuple slots_;
+    py::object first_;
+    int64_t dev_, n_samples_;
+    bool target_observed_;
+    FoldRing<FoldHipOps> ring_;
+};
+
+// ---- CPU test double of the folded ring: Python callbacks
+//   launch(set, index, payload, fold_payload or None, fold_set, fold_index) -> consumed (bool)
+//   exchange(set, n), scale([(payload, set, index), ...], on_comm), wait_set(set),
+//   mark_set(set, on_comm), handoff(), join()
+struct PyFoldOps {
+    using Item = py::object;
+    using P = FoldPending<py::object>;
+    py::object cb;
+    void wait_set(int set) { cb.attr("wait_set")(set); }
+    void mark_set(int set, bool on_comm) { cb.attr("mark_set")(set, on_comm); }
+    void handoff() { cb.attr("handoff")(); }
+    int exchange(int set, int nb) { return cb.attr("exchange")(set, nb).cast<int>(); }
+    int scale(const std::vector<const P*>& run, bool on_comm) {
+        py::list l;
+        for (auto* p : run) l.append(py::make_tuple(p->item, p->set, p->index));
+        return cb.attr("scale")(l, on_comm).cast<int>();
+    }
+    void folded(const P&) {}
+    void join() { cb.attr("join")(); }
+};
+
+class CpuFoldRing {
+  public:
+    CpuFoldRing(py::object cb, int group) : ring_(PyFoldOps{cb}, group) {}
+    int step(py::object payload) {
+        py::object cb = ring_.ops().cb;
+        return ring_.step(
+            [&](Slot s, const FoldPending<py::object>* f, bool& consumed) -> int {
+                consumed = cb.attr("launch")(s.half, s.index, payload, f ? f->item : py::none(), f ? f->set : -1,
+                                             f ? f->index : -1)
+                               .cast<bool>() &&
+                           f != nullptr;
+                return 0;
+            },
+            payload);
+    }
+    int wait() { return ring_.wait(); }
+    int unfinished() const { return ring_.unfinished(); }
+    int group() const { return ring_.group(); }
+
+  private:
+    FoldRing<PyFoldOps> ring_;
+};
+
 // ------------------------------------------------------ redrawn sample domains --
 // A plan whose sample domains are redrawn on every call (N > |domain|: the
 // reference pads the domain with random.uniform draws and sorts, node.py:
@@ -627,6 +986,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("steps", &Stepper::steps)
         .def("group", &Stepper::group)
         .def("host_timing", &Stepper::host_timing);
+    py::class_<FoldStepper>(m, "FoldStepper")
+        .def(py::init<uintptr_t, uintptr_t, uintptr_t, py::tuple, py::object, int64_t, int64_t, bool, int64_t, int,
+                      uintptr_t>())
+        .def("step", &FoldStepper::step)
+        .def("wait", &FoldStepper::wait)
+        .def("synchronize", &FoldStepper::synchronize)
+        .def("steps", &FoldStepper::steps)
+        .def("group", &FoldStepper::group)
+        .def("unfinished", &FoldStepper::unfinished);
+    py::class_<CpuFoldRing>(m, "CpuFoldRing")
+        .def(py::init<py::object, int>())
+        .def("step", &CpuFoldRing::step)
+        .def("wait", &CpuFoldRing::wait)
+        .def("unfinished", &CpuFoldRing::unfinished)
+        .def("group", &CpuFoldRing::group);
     py::class_<CpuStepRing>(m, "CpuStepRing")
         .def(py::init<py::object, int>())
         .def("step", &CpuStepRing::step)

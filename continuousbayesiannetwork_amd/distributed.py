@@ -19,6 +19,8 @@ import torch.distributed as dist
 
 from .base.parameter_learning import GENERATION
 
+_RAW = 8  # CBN_RUN_RAW (include/cbn_amd.h)
+
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     """Contiguous, balanced [lo, hi) slice of n queries for ``rank``."""
@@ -232,8 +234,12 @@ class ShardedStepper:
     """
 
     def __init__(self, bn, target_node: str, N_max: int = 16, group=None, exchange_every: int = 4,
-                 force_exchange: bool = False, gather: bool = False):
+                 force_exchange: bool = False, gather: bool = False, fold: bool = True):
         self.bn, self.target, self.N_max, self.group = bn, target_node, N_max, group
+        # rank-local steps on staged plans: each step's division by its global
+        # max runs inside a later raw launch (cbn_plan_run_fold, FoldStepper)
+        # instead of a separate scale launch
+        self.fold = fold
         self.G = max(1, min(8, exchange_every))
         # force_exchange: all-reduce even at world size 1 (exercises RCCL on one GPU)
         multi = dist.is_initialized() and dist.get_world_size(group) > 1
@@ -245,6 +251,7 @@ class ShardedStepper:
         self._fp = None
         self._comm = 0
         self._serial = False
+        self._folded = False
         self._epoch = None  # engine.epoch the native stepper's plan handle belongs to
 
     def _setup(self, evidence_shard) -> bool:
@@ -271,10 +278,18 @@ class ShardedStepper:
                 world, rank, uid = 1, 0, host.nccl_unique_id(rccl)
             self._comm = host.nccl_comm_init(rccl, uid, world, rank, fp.device.index)
         plan = fp.plan
-        scale_batch = ctypes.cast(_native.load().cbn_scale_batch, ctypes.c_void_p).value
-        self._c = host.Stepper(fp.run_fn, scale_batch, plan.handle.value, fp.slot_keys, fp.first, fp.device.index,
-                               plan.n_samples, plan.target_observed, int(fp.words.numel()), self.G, self._comm,
-                               self.world, self.rank)
+        lib = _native.load()
+        scale_batch = ctypes.cast(lib.cbn_scale_batch, ctypes.c_void_p).value
+        self._folded = (self.fold and not self.gather and int(fp.words.numel()) <= 256
+                        and bool(lib.cbn_plan_flags(plan.handle) & _native.CBN_PLAN_STAGED))
+        if self._folded:
+            self._c = host.FoldStepper(ctypes.cast(lib.cbn_plan_run_fold, ctypes.c_void_p).value, scale_batch,
+                                       plan.handle.value, fp.slot_keys, fp.first, fp.device.index, plan.n_samples,
+                                       plan.target_observed, int(fp.words.numel()), self.G, self._comm)
+        else:
+            self._c = host.Stepper(fp.run_fn, scale_batch, plan.handle.value, fp.slot_keys, fp.first,
+                                   fp.device.index, plan.n_samples, plan.target_observed, int(fp.words.numel()),
+                                   self.G, self._comm, self.world, self.rank)
         self._fp = fp
         return True
 
@@ -295,6 +310,28 @@ class ShardedStepper:
         [Q, N] tensor (Q = ``total_rows``, the whole batch split by
         ``shard_bounds``; None = equal shards), otherwise this rank's rows."""
         eng = self.bn.engine
+        c = self._c
+        if c is not None and GENERATION[0] == eng._gen and eng.epoch == self._epoch and self._folded:
+            # hot path (rank-local, folded): one native call
+            fp = self._fp
+            res = c.step(evidence_shard, out, eng._flags(fp.plan) | _RAW)
+            if type(res) is torch.Tensor:
+                tdom = fp.tdom.get(res.shape[0])
+                return res, (tdom if tdom is not None else self._tdom(fp, res.shape[0]))
+            if res is not None:  # an error code: the step is enqueued (zero words), report it
+                from . import _native
+
+                _native.check(res, "cbn_plan_run_fold")
+        return self._step_slow(evidence_shard, out, total_rows)
+
+    @staticmethod
+    def _tdom(fp, m: int):
+        plan = fp.plan
+        t = fp.tdom[m] = plan.target_domain.unsqueeze(0).expand(m if plan.target_observed else 1, -1)
+        return t
+
+    def _step_slow(self, evidence_shard, out, total_rows):
+        eng = self.bn.engine
         if GENERATION[0] != eng._gen:
             eng._check_generation()  # drops this network's plans if one of its estimators changed
         if self._c is not None and eng.epoch != self._epoch:
@@ -310,28 +347,28 @@ class ShardedStepper:
                                  out=out)
         fp = self._fp
         n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
-        counts = self._counts(n, total_rows)
-        flags = self.bn.engine.raw_flags(fp.plan)
-        res = self._c.step(evidence_shard, out, flags, counts)
+        flags = eng.raw_flags(fp.plan)
+        counts = None if self._folded else self._counts(n, total_rows)
+
+        def native_step(ev):
+            return self._c.step(ev, out, flags) if self._folded else self._c.step(ev, out, flags, counts)
+
+        res = native_step(evidence_shard)
         if res is None:  # dtype / device / layout the native checks reject: convert, same ring
             cols = {k: evidence_shard[k] for k in fp.slot_keys}
             conv = {k: v.to(device=fp.device, dtype=torch.float32).contiguous() for k, v in cols.items()}
             for k, v in conv.items():
                 if v.dim() != 2:
                     raise AssertionError("Each query tensor must be of dimension 2.")
-            res = self._c.step(conv, out, flags, counts)
+            res = native_step(conv)
             if res is None:
                 raise ValueError("ShardedStepper.step: evidence batch rejected (shape / target-unobserved batch > 1)")
         if type(res) is int:
             from . import _native
 
             _native.check(res, "cbn_plan_run(raw)")
-        m = res.shape[0]
-        tdom = fp.tdom.get(m)
-        if tdom is None:
-            plan = fp.plan
-            tdom = fp.tdom[m] = plan.target_domain.unsqueeze(0).expand(m if plan.target_observed else 1, -1)
-        return res, tdom
+        tdom = fp.tdom.get(res.shape[0])
+        return res, (tdom if tdom is not None else self._tdom(fp, res.shape[0]))
 
     def wait(self):
         """Make the current stream wait for every enqueued exchange + scale (+ gathers)."""

@@ -4,7 +4,7 @@ Mirrors cbn/parameter_learning/brute_force.py (same class name, constructor,
 ``fit`` / ``get_prob`` / ``sample`` semantics and error behaviour).  What
 changes is the representation: the reference keeps the unique
 ``[parents..., node, prob]`` rows (``mle_tensor``, :55-66) and answers every
-``get_prob`` with two equality scans over all rows (:240-254, O(points x rows)).
+``get_prob`` with two equality scans over all rows (:227-241, O(points x rows)).
 Here ``fit`` also compiles the rows into a dense conditional table
 ``cpd[parent idx..., node idx] = joint / (parent marginal + 1e-10)`` by the HIP
 kernels ``k_cpd_scatter`` / ``k_cpd_normalize`` (``cbn_bf_cpd_build``), and
@@ -43,7 +43,7 @@ def sparse_conditionals(cell: torch.Tensor, probs: torch.Tensor, card_node: int,
     """Value of each unique row of a hashed CPD (cell = mixed-radix domain
     index, node column last): joint / (parent marginal + 1e-10), the sums of
     brute_force.py:227-241 over the rows sharing the row's parent values; the
-    root case (:205-214) keeps the joint."""
+    root case (:192-201) keeps the joint."""
     if not conditional:
         return probs.clone()
     pcell = torch.div(cell, card_node, rounding_mode="floor")
@@ -170,7 +170,7 @@ class BruteForce(BaseParameterLearningEstimator):
     def _build_sparse(self, lib, dev, cell: torch.Tensor, probs: torch.Tensor, card_node: int, conditional: bool):
         """Hashed CPD: value of unique row u = joint_u / (sum of joint over the
         rows sharing u's parent values + 1e-10) (brute_force.py:227-241), the
-        root case without the division (:205-214)."""
+        root case without the division (:192-201)."""
         vals = sparse_conditionals(cell, probs, card_node, conditional)
         n = cell.numel()
         cap = hash_capacity(n)

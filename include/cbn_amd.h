@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define CBN_AMD_ABI_VERSION 3
+#define CBN_AMD_ABI_VERSION 4
 
 #define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
 #define CBN_MAX_EVIDENCE 256 /* distinct evidence columns per query batch        */
@@ -70,8 +70,8 @@ const char* cbn_last_error(void);
  * scans of brute_force.py:227-241 (joint / parent-marginal sums).
  *   cell[r]  : flat index of mle row r in [n_parent_cells, node_card]
  *   prob[r]  : its empirical probability (counts / total)
- *   normalize: 1 -> cpd = joint / (sum_v joint + 1e-10)  (conditional, :253)
- *              0 -> cpd = joint                          (root marginal, :205-214) */
+ *   normalize: 1 -> cpd = joint / (sum_v joint + 1e-10)  (conditional, :240-241)
+ *              0 -> cpd = joint                          (root marginal, :192-201) */
 int cbn_bf_cpd_build(const int32_t* cell, const float* prob, int64_t n_rows,
                      int64_t n_parent_cells, int32_t node_card, int32_t normalize,
                      float* cpd, void* stream);
@@ -215,6 +215,17 @@ int cbn_scale(float* out, int64_t n, const uint32_t* max_bits, int32_t n_max, vo
  * scales several raw launches at once (distributed.ShardedStepper). */
 int cbn_scale_batch(float* const* outs, const int64_t* n_elems, int32_t n_batches, const uint32_t* max_bits,
                     int32_t n_max, void* stream);
+/* A CBN_RUN_RAW launch that also finishes an EARLIER raw launch: divides
+ * fold_rows[0, fold_n_elems) in place by float(max over fold_words[0,
+ * fold_n_words)) -- that step's cbn_scale (bayesian_network.py:296), bit for
+ * bit -- inside this launch, overlapping the products (the pipelined sharded
+ * stepper scales step s in the launch of step s + 2G).  fold_rows NULL: a plain
+ * raw launch.  Staged plans only (CBN_PLAN_STAGED), else CBN_E_UNSUPPORTED;
+ * fold_n_elems % 4 == 0, fold_rows 16-B aligned, 1 <= fold_n_words <= 256.
+ * Added in ABI 4. */
+int cbn_plan_run_fold(cbn_plan* plan, int64_t n_queries, const float* const* evidence, int32_t n_evidence,
+                      uint32_t* max_bits, float* out, float* fold_rows, int64_t fold_n_elems,
+                      const uint32_t* fold_words, int32_t fold_n_words, int32_t flags, void* stream);
 int cbn_plan_status(cbn_plan* plan, int32_t* status);
 
 /* Which kernels serve the plan (bit set): diagnostics / bench labels. */

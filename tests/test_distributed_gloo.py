@@ -430,3 +430,155 @@ def test_sharded_infer_collectives_two_ranks(tmp_path, case):
     assert [e[0] for e in logs[0]] == [e[0] for e in logs[1]]
     if CASES[case][1] == "binary":
         assert sum(e[0] == "broadcast_object_list" for e in logs[0]) == len(STEPS)  # one draw exchange per call
+
+
+# ---------------------------------------------------------------------------
+# folded-scale ring (csrc/host_fast.cpp FoldRing, the rank-local stepper)
+# ---------------------------------------------------------------------------
+class _FoldOps:
+    """CPU stand-in for FoldHipOps: the raw launch is the oracle's unnormalised
+    product, the exchange a gloo all-reduce(MAX), a fold / scale a division.
+    Stream order is modelled: a set's words become readable on the compute
+    side only after a wait_set following its exchange; a launch may not
+    overwrite words that are still to be consumed; every step is divided
+    exactly once."""
+
+    def __init__(self, G, W, ora, target, N):
+        self.G, self.W, self.ora, self.target, self.N = G, W, ora, target, N
+        self.words = torch.zeros((3 * G, W), dtype=torch.int32)
+        self.valid = [set(), set(), set()]  # exchanged words not yet consumed
+        self.comm_pending = [False, False, False]  # a comm op on the set not yet waited by compute
+        self.log = []
+
+    def _div(self, item, s, i):
+        m = np.int32(int(self.words[s * self.G + i].max())).view(np.float32)
+        assert i in self.valid[s], ("words consumed twice or never exchanged", s, i)
+        self.valid[s].discard(i)
+        item["rows"] /= torch.tensor(m)
+        item["scaled"] += 1
+
+    def launch(self, s, i, item, fold, fs, fi):
+        assert not self.valid[s] or i not in self.valid[s], ("overwrites unconsumed words", s, i)
+        if i == 0:
+            assert not self.valid[s], ("group starts in a set with unconsumed words", s)
+        w = self.words[s * self.G + i]
+        w.zero_()
+        ev = item["ev"]
+        n = next(iter(ev.values())).shape[0]
+        consumed = False
+        if n:
+            raw, _ = self.ora.infer_raw(self.target, ev, self.N)
+            item["rows"][:] = torch.tensor(raw)
+            w[0] = int(np.float32(raw.max()).view(np.int32))
+            if fold is not None:
+                assert not self.comm_pending[fs], ("fold before the compute side waited the exchange", fs)
+                self._div(fold, fs, fi)
+                consumed = True
+        self.log.append(("launch", s, i, item["step"], None if fold is None or not consumed else fold["step"]))
+        return consumed
+
+    def exchange(self, s, nb):
+        grp = self.words[s * self.G: s * self.G + nb]
+        dist.all_reduce(grp, op=dist.ReduceOp.MAX)
+        self.valid[s] = set(range(nb))
+        self.log.append(("exchange", s, nb))
+        return 0
+
+    def scale(self, run, on_comm):
+        for item, s, i in run:
+            if not on_comm:
+                assert not self.comm_pending[s]
+            self._div(item, s, i)
+        self.log.append(("scale", on_comm, [it["step"] for it, _, _ in run]))
+        return 0
+
+    def mark_set(self, s, on_comm):
+        if on_comm:
+            self.comm_pending[s] = True
+
+    def wait_set(self, s):
+        self.comm_pending[s] = False
+
+    def handoff(self):
+        self.log.append(("handoff",))
+
+    def join(self):
+        self.comm_pending = [False, False, False]
+        self.log.append(("join",))
+
+
+FOLD_SIZES = [301, 1, 64, 7, 128, 33, 2, 90, 50, 3, 0, 77, 12, 40, 9, 5, 64]  # an empty batch, empty shards
+
+
+def _fold_worker(rank, world, port, G, waits, out_dir):
+    import json
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    from helpers import chain_data, sample_evidence
+    from oracle.ref_infer import OracleBN
+
+    from continuousbayesiannetwork_amd import _native
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data, cols, edges = chain_data(6, 4, 3000, 7, stay=0.6)
+    ora = OracleBN(edges, cols, data)
+    ops = _FoldOps(G, 4, ora, "X5", 4)
+    ring = _native.load_host().CpuFoldRing(ops, G)
+    items = []
+    for k, Q in enumerate(FOLD_SIZES):
+        ev = sample_evidence(data, cols, ["X4", "X2"], max(Q, 1), 40 + k)
+        lo, hi = shard_bounds(Q, world, rank)
+        mine = {c: v[lo:hi] for c, v in ev.items()}
+        it = dict(step=k, ev=mine, rows=torch.zeros((hi - lo, 4)), scaled=0)
+        assert ring.step(it) == 0
+        items.append(it)
+        if k in waits:
+            assert ring.wait() == 0
+            assert ring.unfinished() == 0
+    assert ring.wait() == 0
+    assert ring.unfinished() == 0
+    for it in items:
+        np.save(os.path.join(out_dir, f"f{rank}_s{it['step']}.npy"), it["rows"].numpy())
+        assert it["scaled"] == 1, (it["step"], it["scaled"])
+    with open(os.path.join(out_dir, f"flog{rank}.json"), "w") as fh:
+        json.dump(ops.log, fh)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G,waits", [(2, ()), (3, (5,)), (1, (2, 9)), (4, (12,))])
+def test_fold_ring_two_ranks(tmp_path, G, waits):
+    """csrc/host_fast.cpp FoldRing (the rank-local ShardedStepper with the
+    scale folded into later raw launches) over gloo with the oracle as the
+    device: groups of G, wait() mid-stream, an empty batch and empty shards,
+    uneven shards -> every rank's rows equal the unsharded oracle's rows,
+    every step is divided exactly once, launches fold only exchanged and
+    waited words, never overwrite words still to be consumed, and both ranks
+    issue the same all-reduces."""
+    import json
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    from helpers import chain_data, sample_evidence
+    from oracle.ref_infer import OracleBN
+
+    mp.spawn(_fold_worker, args=(2, _free_port(), G, waits, str(tmp_path)), nprocs=2, join=True)
+    data, cols, edges = chain_data(6, 4, 3000, 7, stay=0.6)
+    ora = OracleBN(edges, cols, data)
+    for k, Q in enumerate(FOLD_SIZES):
+        if Q == 0:
+            continue
+        ref, _ = ora.infer("X5", sample_evidence(data, cols, ["X4", "X2"], Q, 40 + k), 4)
+        for r in range(2):
+            lo, hi = shard_bounds(Q, 2, r)
+            np.testing.assert_array_equal(np.load(tmp_path / f"f{r}_s{k}.npy"), ref[lo:hi])
+    logs = [json.load(open(tmp_path / f"flog{r}.json")) for r in range(2)]
+    assert [e for e in logs[0] if e[0] == "exchange"] == [e for e in logs[1] if e[0] == "exchange"]
+    folds = [e for e in logs[0] if e[0] == "launch" and e[4] is not None]
+    assert folds, "no step was folded into a later launch"
+    for e in folds:
+        assert e[3] - e[4] >= 2 * G - (G - 1)  # a fold reaches at least one whole group back

@@ -369,8 +369,9 @@ def test_raw_launch_sharded_equals_single_launch(Q, shards, gpu):
     np.testing.assert_array_equal(one.cpu().numpy(), full.cpu().numpy())
 
 
-@pytest.mark.parametrize("every,exchange", [(1, False), (2, True), (3, False), (4, True), (8, True)])
-def test_sharded_stepper_pipelined_equals_infer(every, exchange, gpu):
+@pytest.mark.parametrize("every,exchange,fold", [(1, False, True), (2, True, True), (3, False, True), (4, True, True),
+                                                 (8, True, True), (2, True, False), (8, True, False)])
+def test_sharded_stepper_pipelined_equals_infer(every, exchange, fold, gpu):
     """ShardedStepper (raw launch on the compute stream; exchange + batched
     scale of every ``every`` steps on its comm stream; ring of max-word slots)
     over a stream of distinct batches (7 per pass: partial groups flushed by
@@ -384,7 +385,7 @@ def test_sharded_stepper_pipelined_equals_infer(every, exchange, gpu):
     batches = [_t(sample_evidence(data, cols, names, 4096 + 1000 * i, 30 + i), gpu) for i in range(7)]
     ref = [bn.infer("X19", b, N_max=32)[0].clone() for b in batches]
     # exchange: a one-rank RCCL communicator of the stepper's own (no process group)
-    st = ShardedStepper(bn, "X19", 32, exchange_every=every, force_exchange=exchange)
+    st = ShardedStepper(bn, "X19", 32, exchange_every=every, force_exchange=exchange, fold=fold)
     keep = []
     for rep in range(3):
         for i, b in enumerate(batches):
@@ -393,6 +394,7 @@ def test_sharded_stepper_pipelined_equals_infer(every, exchange, gpu):
                 keep.append((i, rows))  # odd steps' rows are dropped right away
     st.wait()
     torch.cuda.synchronize()
+    assert st._folded == fold  # staged plan: the folded ring unless disabled
     st.close()
     for i, rows in keep:
         np.testing.assert_array_equal(rows.cpu().numpy(), ref[i].cpu().numpy())
@@ -637,3 +639,40 @@ def test_redrawn_domains_on_the_sharded_path(gpu):
             torch.cuda.synchronize()
             st.close()
             np.testing.assert_array_equal(c.cpu().numpy(), a.cpu().numpy())
+
+
+@pytest.mark.parametrize("Q0,Q1", [(65536, 65536), (4096, 65536), (65536, 1000), (7, 3)])
+def test_raw_launch_with_folded_scale(Q0, Q1, gpu):
+    """cbn_plan_run_fold: a raw launch of batch 1 that also divides batch 0's
+    raw rows by batch 0's max words (bayesian_network.py:296 for that batch):
+    batch 1's raw rows and words equal a plain raw launch's, and batch 0's
+    rows equal the single-process infer bit for bit (both batch-size orders:
+    the fold slice per block differs from the launch's own)."""
+    import ctypes
+
+    from continuousbayesiannetwork_amd import _native
+
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    e0 = _t(sample_evidence(data, cols, names, Q0, 71), gpu)
+    e1 = _t(sample_evidence(data, cols, names, Q1, 72), gpu)
+    ref0 = bn.infer("X19", e0, N_max=32)[0].clone()
+    rows1, _, w1, sc1 = bn.engine.infer_raw("X19", e1, 32)
+    rows1, w1 = rows1.clone(), w1.clone()
+    rows0, _, w0, _ = bn.engine.infer_raw("X19", e0, 32)
+    rows0, w0 = rows0.clone(), w0.clone()
+    plan = next(iter(bn.engine._plans.values()))
+    assert _native.load().cbn_plan_flags(plan.handle) & _native.CBN_PLAN_STAGED
+    fp = bn.engine.raw_fast_path("X19", e1, 32)
+    ptrs = (ctypes.c_void_p * len(fp.slot_keys))(*[e1[k].data_ptr() for k in fp.slot_keys])
+    out1 = torch.empty_like(rows1)
+    words = torch.zeros_like(w1)
+    rc = _native.load().cbn_plan_run_fold(plan.handle, Q1, ptrs, len(fp.slot_keys), words.data_ptr(),
+                                          out1.data_ptr(), rows0.data_ptr(), rows0.numel(), w0.data_ptr(),
+                                          w0.numel(), 0, _native.stream_ptr(gpu))
+    _native.check(rc, "cbn_plan_run_fold")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out1.cpu().numpy(), rows1.cpu().numpy())
+    np.testing.assert_array_equal(words.cpu().numpy(), w1.cpu().numpy())
+    np.testing.assert_array_equal(rows0.cpu().numpy(), ref0.cpu().numpy())

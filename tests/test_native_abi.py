@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     lib = _native.load()
-    assert lib.cbn_abi_version() == 3 == _native.ABI_VERSION
+    assert lib.cbn_abi_version() == 4 == _native.ABI_VERSION
     # cbn_factor_desc: 3 int32 + 2*8 int32 + 3 pointers + 8 pointers (with alignment padding)
     assert ctypes.sizeof(_native.FactorDesc) == 4 * 19 + 4 + 8 * 11
     # cbn_param_model: 8 int32 (family, n_layers, width[5], act) + pointer + 2 float + widths pointer

@@ -72,10 +72,14 @@ st0.close()
 st1 = ShardedStepper(bn, "X19", 32, exchange_every=1, force_exchange=True)
 report("pipelined ShardedStepper.step, exchange every step", lambda: st1.step(ev), 2000)
 st1.close()
-st = ShardedStepper(bn, "X19", 32, force_exchange=True)
+for fold in (False, True):
+    st2 = ShardedStepper(bn, "X19", 32, force_exchange=True, exchange_every=8, fold=fold)
+    report(f"pipelined ShardedStepper.step, groups of 8, fold={fold}", lambda: st2.step(ev), 2000)
+    st2.close()
+st = ShardedStepper(bn, "X19", 32, force_exchange=True, fold=False)
 report("pipelined ShardedStepper.step", lambda: st.step(ev), 2000)
 flags = bn.engine.raw_flags(st._fp.plan)
-report("native Stepper.step called directly", lambda: st._c.step(ev, None, flags), 2000)
+report("native Stepper.step called directly", lambda: st._c.step(ev, None, flags, None), 2000)
 if rank == 0:
     names = ["gather+alloc", "raw launch", "exchange share + return"]
     print("  native step phases (us):", {k: round(v, 2) for k, v in zip(names, st._c.host_timing())}, flush=True)
