@@ -1264,8 +1264,13 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     float acc[8];
     long long fq = -1;
     int buf = 0;
+    // write-through stores (sc1: nothing left dirty in L2 for the end-of-kernel
+    // release to write back): the fused launch's final rows, and a folding raw
+    // launch's rows (read again only two groups later, never L2 hits)
+    const bool wt_raw = MODE == kModeRaw && fold.rows != nullptr;  // kernel-uniform
     const __amdgpu_buffer_rsrc_t orsrc =
-        rows_rsrc(MODE != kModeFused ? nullptr : out + q0 * N, MODE != kModeFused ? 0 : (q1 - q0) * (long long)(N * 4));
+        rows_rsrc((MODE == kModeFused || wt_raw) ? out + q0 * N : nullptr,
+                  (MODE == kModeFused || wt_raw) ? (q1 - q0) * (long long)(N * 4) : 0);
     for (; qr < q1; qr += kSR, buf ^= 1) {  // block-uniform
         const long long qn = qr + kSR;
         // next round's evidence flies during these products (the fused launch has one round)
@@ -1338,7 +1343,11 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         CBN_STAMP(5);
         if (q < q1) {
             if (MODE == kModeFused) fq = q;
-            if (MODE == kModeWrite || MODE == kModeRaw) {
+            if (MODE == kModeRaw && wt_raw) {
+                const int ob = (int)(q - q0) * (N * 4);
+                store_wt(orsrc, ob + clo * 4, make_float4(acc[0], acc[1], acc[2], acc[3]));
+                store_wt(orsrc, ob + chi * 4, make_float4(acc[4], acc[5], acc[6], acc[7]));
+            } else if (MODE == kModeWrite || MODE == kModeRaw) {
                 // plain stores: the raw rows are re-read by the scale pass (L2 hits)
                 const float dv = MODE == kModeWrite ? maxv : 1.f;
                 float* o = out + q * N;
@@ -1366,12 +1375,14 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
         m = wave_max_u(m);
         const double y = 1.0 / (double)__uint_as_float(m);  // acc / max correctly rounded (see the fused epilogue)
         float4* r4 = reinterpret_cast<float4*>(fold.rows);
+        const __amdgpu_buffer_rsrc_t frsrc = rows_rsrc(fold.rows + fb * 4, fe > fb ? (fe - fb) * 16 : 0);  // (write-through)
 #pragma unroll
         for (int k = 0; k < kFoldK; ++k) {
             const long long i = fb + tid + k * kQueryThreads;
             if (i < fe)
-                r4[i] = make_float4((float)((double)fv[k].x * y), (float)((double)fv[k].y * y),
-                                    (float)((double)fv[k].z * y), (float)((double)fv[k].w * y));
+                store_wt(frsrc, (int)(i - fb) * 16,
+                         make_float4((float)((double)fv[k].x * y), (float)((double)fv[k].y * y),
+                                     (float)((double)fv[k].z * y), (float)((double)fv[k].w * y)));
         }
         // a slice beyond kFoldK float4 per thread (batches larger than the launch's grid x 2048)
         for (long long i = fb + tid + kFoldK * kQueryThreads; i < fe; i += kQueryThreads) {

@@ -300,7 +300,11 @@ struct HipOps {
     hipStream_t A() const { return c10::hip::getCurrentHIPStream(dev).stream(); }
     int* slot_words(Slot s) { return words.data_ptr<int>() + ((int64_t)s.half * G + s.index) * W; }
 
-    void wait_done(int half) { CBN_HIP_OK(hipStreamWaitEvent(A(), done_ev[half], 0)); }
+    // (an event that already completed needs no wait packet: a stream wait
+    // costs the queue a barrier packet per group even when satisfied)
+    void wait_done(int half) {
+        if (hipEventQuery(done_ev[half]) != hipSuccess) CBN_HIP_OK(hipStreamWaitEvent(A(), done_ev[half], 0));
+    }
     void handoff() {
         CBN_HIP_OK(hipEventRecord(ready, A()));
         CBN_HIP_OK(hipStreamWaitEvent(cs.stream(), ready, 0));
@@ -734,8 +738,9 @@ struct FoldHipOps {
     hipStream_t A() const { return c10::hip::getCurrentHIPStream(dev).stream(); }
     int* slot_words(int set, int index) { return words.data_ptr<int>() + ((int64_t)set * G + index) * W; }
 
-    void wait_set(int set) {
-        if (set_used[set]) CBN_HIP_OK(hipStreamWaitEvent(A(), set_ev[set], 0));
+    void wait_set(int set) {  // (skipped when the event already completed, as HipOps::wait_done)
+        if (set_used[set] && hipEventQuery(set_ev[set]) != hipSuccess)
+            CBN_HIP_OK(hipStreamWaitEvent(A(), set_ev[set], 0));
     }
     void mark_set(int set, bool on_comm) {
         CBN_HIP_OK(hipEventRecord(set_ev[set], on_comm ? cs.stream() : A()));

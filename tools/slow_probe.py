@@ -1,0 +1,55 @@
+"""Diagnostic: per-step wall time of the fused infer and of the sharded
+stepper (with and without an RCCL communicator), several rounds each, in one
+process, in this order -- to see which one, and when, runs slow."""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from continuousbayesiannetwork_amd import BayesianNetwork  # noqa: E402
+from continuousbayesiannetwork_amd.distributed import ShardedStepper  # noqa: E402
+from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+data, cols, edges = chain_data(20, 32, 200_000, 3, stay=0.8)
+bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
+names = [c for c in cols if c != "X19"]
+evs = [{k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, 65536, 1000 + i).items()}
+       for i in range(16)]
+K = 400
+T0 = time.perf_counter()
+
+
+def rounds(name, fn, after=None, n=3):
+    for r in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(K):
+            fn(evs[i % len(evs)])
+        t1 = time.perf_counter()
+        if after:
+            after()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"t={t0 - T0:7.3f} {name} r{r}: enqueue {(t1 - t0) / K * 1e6:6.2f} wall {(t2 - t0) / K * 1e6:6.2f} us/step",
+              flush=True)
+
+
+def stepper(comm, fold):
+    st = ShardedStepper(bn, "X19", 32, force_exchange=comm, exchange_every=8, fold=fold)
+    rounds(f"stepper comm={comm} fold={fold}", lambda e: st.step(e), st.wait)
+    st.close()
+
+
+for what in sys.argv[1:]:
+    if what == "fused":
+        rounds("fused", lambda e: bn.infer("X19", e, N_max=32))
+    else:
+        comm, fold = what.split(",")
+        stepper(comm == "comm", fold == "fold")
