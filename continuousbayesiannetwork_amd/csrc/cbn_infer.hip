@@ -1654,11 +1654,23 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     return CBN_OK;
 }
 
+// CUs a raw launch leaves free (CBN_RAW_RESERVE_CU, diagnostic A/B knob): room
+// for a concurrently running collective's workgroups, so no block of the raw
+// launch waits for one to finish
+int raw_reserve_cu() {
+    static int v = [] {
+        const char* e = getenv("CBN_RAW_RESERVE_CU");
+        const int x = e ? atoi(e) : 0;
+        return x >= 0 && x <= 64 ? x : 0;
+    }();
+    return v;
+}
+
 template <int VPL, bool LDS>
 int launch_raw_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s,
                  const FoldJob* fold = nullptr) {
     const int L = p->N / (4 * VPL);
-    const long long cap = p->max_slots;
+    const long long cap = std::max(1, p->max_slots - raw_reserve_cu());
     long long blocks = (Q * L + kQueryThreads - 1) / kQueryThreads;
     if (blocks > cap) blocks = cap;
     launch_fast_k<VPL, LDS, kModeRaw>(p, (unsigned)blocks, s, ev, Q, L, 0u, nullptr, p->max_slots, max_bits, out,

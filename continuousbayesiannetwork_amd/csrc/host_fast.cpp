@@ -106,6 +106,19 @@ using scale_batch_fn = int (*)(float* const*, const int64_t*, int32_t, const uns
         if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+// The stepper's comm stream: a pooled stream of NORMAL priority.  Measured
+// (tools/slow_probe.py, profiles/r03_stepper_probe.txt): with the first pooled
+// high-priority stream as the comm stream, the raw launches on the compute
+// stream ran at ~52 us per step instead of ~12.5 for as long as the stepper
+// lived.  CBN_COMM_HIGH_PRIO=1 restores the high-priority stream (A/B).
+c10::hip::HIPStream comm_stream(c10::DeviceIndex dev) {
+    static const bool high = [] {
+        const char* e = getenv("CBN_COMM_HIGH_PRIO");
+        return e && e[0] == '1';
+    }();
+    return c10::hip::getStreamFromPool(high, dev);
+}
+
 // ---------------------------------------------------------------- RCCL comm --
 // A communicator of our own (not c10d's): the sharded step's all-reduce is
 // enqueued on the stepper's comm stream straight from C++.  The entry points
@@ -278,7 +291,7 @@ struct HipOps {
 
     HipOps(scale_batch_fn sb, ncclComm_t c, int world_, int rank_, int64_t dev_, int64_t W_, int G_)
         : scale_batch(sb), comm(c), world(world_), rank(rank_), dev(dev_), W(W_), G(G_),
-          cs(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)dev_)) {
+          cs(comm_stream((c10::DeviceIndex)dev_)) {
         words = at::zeros({2 * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
         CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));
@@ -713,7 +726,7 @@ struct FoldHipOps {
 
     FoldHipOps(scale_batch_fn sb, ncclComm_t c, int64_t dev_, int64_t W_, int G_)
         : scale_batch(sb), comm(c), dev(dev_), W(W_), G(G_),
-          cs(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)dev_)) {
+          cs(comm_stream((c10::DeviceIndex)dev_)) {
         words = at::zeros({kSets * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
         CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));

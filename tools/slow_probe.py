@@ -41,9 +41,37 @@ def rounds(name, fn, after=None, n=3):
               flush=True)
 
 
-def stepper(comm, fold):
+_blk = None
+
+
+def blocker(n_blocks):
+    """A stand-in collective kernel on another stream once per group of 8 steps:
+    n_blocks x 256 threads, 40 KB LDS each, ~25 us (tools/probes/blocker.hip)."""
+    global _blk
+    import ctypes
+
+    if _blk is None:
+        _blk = ctypes.CDLL(os.path.join(ROOT, "tools", "probes", "libblocker.so"))
+        _blk.blocker_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p]
+    side = torch.cuda.Stream()
+    count = [0]
+
+    def hook():
+        count[0] += 1
+        if count[0] % 8 == 0:
+            _blk.blocker_launch(n_blocks, 256, 40 * 1024, 25_000, ctypes.c_void_p(side.cuda_stream))
+    return hook
+
+
+def stepper(comm, fold, n_block=0):
     st = ShardedStepper(bn, "X19", 32, force_exchange=comm, exchange_every=8, fold=fold)
-    rounds(f"stepper comm={comm} fold={fold}", lambda e: st.step(e), st.wait)
+    hook = blocker(n_block) if n_block else None
+
+    def step(e):
+        st.step(e)
+        if hook:
+            hook()
+    rounds(f"stepper comm={comm} fold={fold} blocker={n_block}", step, st.wait)
     st.close()
 
 
@@ -51,5 +79,5 @@ for what in sys.argv[1:]:
     if what == "fused":
         rounds("fused", lambda e: bn.infer("X19", e, N_max=32))
     else:
-        comm, fold = what.split(",")
-        stepper(comm == "comm", fold == "fold")
+        parts = what.split(",")
+        stepper(parts[0] == "comm", parts[1] == "fold", int(parts[2]) if len(parts) > 2 else 0)
