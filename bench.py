@@ -224,9 +224,10 @@ def main():
         cpu = cpu_baseline(data, cols, edges, ev_np, target, d, a.cpu_seconds)
     if sharded:
         torch.cuda.set_device(local)
-        if "MASTER_ADDR" not in os.environ:  # --sharded outside torch.distributed.run
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"),
-                              RANK="0", WORLD_SIZE="1")
+        if "WORLD_SIZE" not in os.environ:  # --sharded outside torch.distributed.run: a one-rank group
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(free_port())), ("RANK", "0"),
+                         ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -292,9 +293,10 @@ def main():
     t0 = time.perf_counter()
     ev0.record()  # the library launches on torch's current stream: these events bracket every launch
     for i in range(K):
-        # two-launch path / the sharded step's raw launch: HIP events recorded inside
-        # the library around the launches of every 8th step (on the launch stream)
-        bn.engine.timed = (sharded or not fused) and i % 8 == 7
+        # two-launch path: HIP events recorded inside the library around the
+        # passes of every 8th step (the sharded step is timed over the region:
+        # per-step event records cost it ~3 us per step)
+        bn.engine.timed = not sharded and not fused and i % 8 == 7
         step()
     stepper.wait()
     ev1.record()
@@ -311,7 +313,7 @@ def main():
     value = Q * world * K / sec
 
     roofline = None
-    ntimed, tmax_ms, twrite_ms = bn.engine.timing()
+    ntimed, tmax_ms, twrite_ms = bn.engine.timing() if not sharded else (0, 0.0, 0.0)
     bn.engine.check_status()
     if fused:
         # one launch per step: average launch duration = HIP-event time of the timed region / K
@@ -329,7 +331,6 @@ def main():
         # the dominant kernel: fused single launch; beyond its capacity the raw
         # compute pass (then an HBM-bound scale); --two-pass: the write pass
         mode, what, t_dom = ((2, "single launch: both passes", twrite) if fused else
-                             (3, "raw launch of the sharded step", twrite) if sharded else
                              (1, "write pass", twrite) if a.two_pass else (3, "raw compute pass", tmax))
         kname = (f"k_query_staged<{mode}>" if pflags & _native.CBN_PLAN_STAGED
                  else f"k_query_fast<{vpl}, true, {mode}, {nptr}>")  # <MODE> / <VPL, LDS, MODE, NP>
@@ -342,7 +343,7 @@ def main():
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
         roofline["timing"] = ("HIP events on the launch stream around the whole timed region / K launches" if fused
                               else "HIP events around the launches of every 8th step (library-side)")
-        if not fused and not sharded:
+        if not fused:
             roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
     step_info = None
     if sharded and gather and world > 1:
@@ -358,20 +359,31 @@ def main():
                          avg_us=round(t_step * 1e6, 2), bytes_per_step=bytes_in,
                          timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
                                 "rows received from the other ranks per step")
+        roofline = dict(step_info, kernel=step_info["what"], traffic=None, algorithmic_bytes_per_launch=bytes_in,
+                        timed_steps=K)
     elif sharded:
-        # sharded step (raw launch + all-reduce(max) of the block words + in-place
-        # scale, overlapped across steps): per-GPU algorithmic bytes of one step =
-        # evidence in + raw rows out + the scale's read and write of the rows,
-        # over this rank's HIP-event step time on the launch stream
+        # rank-local sharded step: ONE raw launch per step on the launch stream,
+        # which also divides an earlier step's rows by that step's all-reduced
+        # max (cbn_plan_run_fold; the group's all-reduce runs on the comm
+        # stream); algorithmic bytes of that launch = evidence in + raw rows out
+        # + the folded rows read and written back; duration = HIP events on
+        # the launch stream around the timed region / K (an upper bound on the
+        # launch: it includes the step's share of the launch gaps)
         n_cols = len(names)
         bytes_step = Q * (4 * n_cols + 3 * 4 * d)
         t_step = ev0.elapsed_time(ev1) / K * 1e-3
         achieved = bytes_step / t_step / 1e9
-        step_info = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                         frac=round(achieved / HBM_PEAK_GBS, 4),
-                         what="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch (per step)",
-                         avg_us=round(t_step * 1e6, 2), bytes_per_step=bytes_step,
-                         timing="HIP events on rank 0's launch stream around the timed region / K steps")
+        folded = getattr(stepper, "_folded", False)
+        kname = "k_query_staged<3>"
+        traffic, tsrc = pmc_traffic(kname)
+        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        kernel=kname + (" (raw launch with an earlier step's scale folded in)" if folded
+                                        else " (raw launch; k_scale_batch on the comm stream per group)"),
+                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_step, timed_steps=K,
+                        timing="HIP events on the launch stream around the timed region / K steps")
+        if tsrc:
+            roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
 
     other = None
     if sharded:
@@ -414,7 +426,6 @@ def main():
                                " + RCCL all-gather of the [Q, N] marginal tensor on every rank" if gather else "")
                            if sharded else "")},
             "roofline": roofline, "cpu_baseline": cpu,
-            **({"sharded_step": step_info} if step_info else {}),
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
             "evidence_batches": len(batches),
         }

@@ -21,7 +21,7 @@ data, cols, edges = chain_data(20, 32, 200_000, 3, stay=0.8)
 bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
 names = [c for c in cols if c != "X19"]
 evs = [{k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, 65536, 1000 + i).items()}
-       for i in range(16)]
+       for i in range(int(os.environ.get("NB", "16")))]
 K = 400
 T0 = time.perf_counter()
 
@@ -76,6 +76,17 @@ def stepper(comm, fold, n_block=0):
 
 
 for what in sys.argv[1:]:
+    if what in ("pg_nccl", "pg_gloo"):  # a torch process group first, as bench.py has one
+        import torch.distributed as dist
+
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29541"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+        if what == "pg_nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        print(f"t={time.perf_counter() - T0:7.3f} {what} initialised", flush=True)
+        continue
     if what == "fused":
         rounds("fused", lambda e: bn.infer("X19", e, N_max=32))
     else:
