@@ -102,6 +102,8 @@ def parse():
                          "rank as `value`; by default each rank keeps its normalised shard of the marginal tensor "
                          "(the reassembly cannot scale: DESIGN.md, Multi-GPU) and the gathered step is measured "
                          "after it and reported as value_gathered")
+    ap.add_argument("--skip-other", action="store_true",
+                    help="N>1: do not time the other reassembly choice after the headline step (profiling runs)")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
@@ -386,7 +388,7 @@ def main():
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
 
     other = None
-    if sharded:
+    if sharded and not a.skip_other:
         # the same step with the other reassembly choice, for reference: the
         # all-gather of the full [Q, N] tensor on every rank (value_gathered), or
         # (with --gather) each rank keeping its rows (value_rank_local)

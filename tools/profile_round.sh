@@ -21,9 +21,9 @@ run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fe
 run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline
 run summary 120 python tools/profile_summary.py --tag $TAG --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 40)"
 run prof_sh 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sh -o run --output-format csv -- python3 bench.py --no-cpu-baseline --sharded
-run pmc_sh_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_sh_fetch -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline --sharded
-run pmc_sh_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_sh_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 4 --no-cpu-baseline --sharded
-run summary_sh 120 python tools/profile_summary.py --tag ${TAG}_sharded --prof gpurun_out/prof_sh --fetch gpurun_out/pmc_sh_fetch --write gpurun_out/pmc_sh_write --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --sharded (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 40)"
+run pmc_sh_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_sh_fetch -o run --output-format csv -- python3 bench.py --steps 200 --warmup 4 --no-cpu-baseline --sharded --skip-other
+run pmc_sh_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_sh_write -o run --output-format csv -- python3 bench.py --steps 200 --warmup 4 --no-cpu-baseline --sharded --skip-other
+run summary_sh 120 python tools/profile_summary.py --tag ${TAG}_sharded --prof gpurun_out/prof_sh --fetch gpurun_out/pmc_sh_fetch --write gpurun_out/pmc_sh_write --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --sharded (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 200 --warmup 4 --skip-other: 204 raw launches, the first 16 without a fold)"
 run bench_final 600 python bench.py
 run bench_sharded_final 300 python bench.py --sharded --no-cpu-baseline
 echo "session done"
