@@ -106,6 +106,15 @@ using scale_batch_fn = int (*)(float* const*, const int64_t*, int32_t, const uns
         if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+// The steppers' cross-stream events order the two streams of ONE device (the
+// comm stream's all-reduce reads words the compute stream's launches wrote;
+// RCCL fences its own peer traffic), so a device-scope release is enough.  The
+// default system-scope fence writes back and invalidates L2 at every record:
+// measured, the compute stream lost ~20 us per group of 8 steps to the group's
+// two records (no-comm folded stepper 13.0-13.4 -> 10.6-10.9 us per step
+// without them, tools/slow_probe.py).
+constexpr unsigned kEvFlags = hipEventDisableTiming | hipEventReleaseToDevice;
+
 // The stepper's comm stream: a pooled stream of NORMAL priority.  Measured
 // (tools/slow_probe.py, profiles/r03_stepper_probe.txt): with the first pooled
 // high-priority stream as the comm stream, the raw launches on the compute
@@ -293,9 +302,9 @@ struct HipOps {
         : scale_batch(sb), comm(c), world(world_), rank(rank_), dev(dev_), W(W_), G(G_),
           cs(comm_stream((c10::DeviceIndex)dev_)) {
         words = at::zeros({2 * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
-        CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));
-        for (auto& e : done_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        CBN_HIP_OK(hipEventCreateWithFlags(&ready, kEvFlags));
+        CBN_HIP_OK(hipEventCreateWithFlags(&tail, kEvFlags));
+        for (auto& e : done_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, kEvFlags));
     }
     HipOps(HipOps&& o) noexcept
         : scale_batch(o.scale_batch), comm(o.comm), world(o.world), rank(o.rank), dev(o.dev), W(o.W), G(o.G),
@@ -573,8 +582,9 @@ int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max)
 //                     folding the oldest unfinished step of a group exchanged
 //                     two groups back (its all-reduce had a whole group of
 //                     launches to complete)
-//   comm stream C:    after each group's last launch, ONE all-reduce(MAX) of
-//                     the group's words in place
+//   comm stream C:    per group, ONE all-reduce(MAX) of the group's words in
+//                     place, enqueued once A has passed the group's last
+//                     launch (host-side event query / wait, no stream wait)
 // Word sets form a ring of kSets groups.  Before a group writes set s, any
 // step whose words are still in s and not yet folded (a group with empty
 // shards or a partial group flushed by wait()) is scaled on A first, and A
@@ -583,6 +593,7 @@ int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max)
 // FoldHipOps binds it to HIP / RCCL / cbn_plan_run_fold, PyFoldOps to Python
 // callbacks (the world-size-2 gloo test drives the same ring on CPU).
 constexpr int kSets = 3;
+constexpr int kFoldGroupMax = 32;
 
 template <class Item>
 struct FoldPending {
@@ -596,14 +607,18 @@ class FoldRing {
   public:
     using Item = typename Ops::Item;
     using Pending = FoldPending<Item>;
-    FoldRing(Ops ops, int group) : ops_(std::move(ops)), G_(group < 1 ? 1 : (group > 8 ? 8 : group)) {}
+    // (groups up to kFoldGroupMax steps: a group's leftovers are scaled in runs of <= 8)
+    FoldRing(Ops ops, int group) : ops_(std::move(ops)), G_(group < 1 ? 1 : (group > kFoldGroupMax ? kFoldGroupMax : group)) {}
 
     // launch(slot, fold, consumed) writes the step's rows and words slot and,
     // when `fold` is non-null and the step launches a kernel, finishes that
     // earlier step (consumed = true).  Returns 0 or a C ABI error code.
     template <class Launch>
     int step(Launch&& launch, Item item) {
-        if (cur_.empty()) begin_group();
+        if (cur_.empty()) {
+            const int brc = begin_group();
+            if (brc) return brc;
+        }
         const int set = (int)(g_ % kSets);
         const Slot slot{set, (int)cur_.size()};
         const Pending* f = foldq_.empty() ? nullptr : &foldq_.front();
@@ -623,6 +638,8 @@ class FoldRing {
     int wait() {
         int rc = exchange_group();
         if (rc) return rc;
+        for (auto& grp : exch_)
+            if (!grp.handed && (rc = hand(grp, /*eager=*/true))) return rc;
         for (auto& grp : exch_)
             for (auto& p : grp.items) foldq_.push_back(std::move(p));
         exch_.clear();
@@ -645,8 +662,38 @@ class FoldRing {
     struct Group {
         int64_t g;
         std::vector<Pending> items;
+        bool handed = false;
     };
-    void begin_group() {
+    // Hand exchanged groups to C, oldest first: a group needed for folding by
+    // this group (exchanged two groups back) now, waiting on the host for A to
+    // pass its last launch; a later one only when A has already passed it.
+    // Either way C's all-reduce needs no stream wait on A: measured, a comm
+    // stream waiting on the compute stream's event slowed the raw launches by
+    // ~2.5 us per step (tools/slow_probe.py, CBN_FOLD_DIAG_SKIP).  eager_
+    // (CBN_FOLD_EAGER=1, A/B) hands each group at its exchange with the wait.
+    int hand_ready() {
+        for (auto& grp : exch_) {
+            if (grp.handed) continue;
+            const int gset = (int)(grp.g % kSets);
+            const bool need = grp.g <= g_ - 2;
+            if (!ops_.passed(gset, /*block=*/need)) break;
+            const int rc = hand(grp, /*eager=*/false);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    int hand(Group& grp, bool eager) {
+        const int gset = (int)(grp.g % kSets);
+        if (eager) ops_.handoff(gset);  // C after A's record of the group's last launch
+        const int rc = ops_.exchange(gset, (int)grp.items.size());
+        if (rc) return rc;
+        ops_.mark_set(gset, /*on_comm=*/true);
+        grp.handed = true;
+        return 0;
+    }
+    int begin_group() {
+        const int hrc = hand_ready();
+        if (hrc) return hrc;
         const int set = (int)(g_ % kSets);
         // steps whose words still sit in `set`: finish them before this group overwrites it
         std::deque<Pending> here, keep;
@@ -661,25 +708,27 @@ class FoldRing {
             }
         }
         ops_.wait_set(set);  // A after C's last use of the set (its exchange / a wait() scale)
-        if (!here.empty()) scale_runs(here, /*on_comm=*/false);
-        // groups exchanged two or more groups back become foldable
+        if (!here.empty()) {
+            const int rc = scale_runs(here, /*on_comm=*/false);
+            if (rc) return rc;
+        }
+        // groups exchanged two or more groups back (handed above) become foldable
         while (!exch_.empty() && exch_.front().g <= g_ - 2) {
             Group& grp = exch_.front();
             if (!grp.items.empty()) ops_.wait_set(grp.items.front().set);  // their all-reduce done
             for (auto& p : grp.items) foldq_.push_back(std::move(p));
             exch_.pop_front();
         }
+        return 0;
     }
     int exchange_group() {
         if (cur_.empty()) return 0;
         const int set = (int)(g_ % kSets);
-        ops_.handoff();  // C after every launch so far (the group's raw launches and their folds)
-        const int rc = ops_.exchange(set, (int)cur_.size());
-        if (rc) return rc;
-        ops_.mark_set(set, /*on_comm=*/true);
+        ops_.record(set);  // A's position after the group's raw launches (and their folds)
         exch_.push_back(Group{g_, std::move(cur_)});
         cur_.clear();
         ++g_;
+        if (eager_) return hand(exch_.back(), /*eager=*/true);
         return 0;
     }
     // scale the given steps (runs of consecutive slots of one set per call)
@@ -700,6 +749,10 @@ class FoldRing {
 
     Ops ops_;
     int G_;
+    bool eager_ = [] {
+        const char* e = getenv("CBN_FOLD_EAGER");
+        return e && e[0] == '1';
+    }();
     std::vector<Pending> cur_;
     std::deque<Group> exch_;
     std::deque<Pending> foldq_;
@@ -720,32 +773,34 @@ struct FoldHipOps {
     int G = 1;
     c10::hip::HIPStream cs;
     at::Tensor words;  // [kSets * G, W] int32 on the device
-    hipEvent_t ready = nullptr, tail = nullptr;
-    hipEvent_t set_ev[kSets] = {};
+    hipEvent_t tail = nullptr;
+    hipEvent_t set_ev[kSets] = {}, ready_ev[kSets] = {};
     bool set_used[kSets] = {};
 
     FoldHipOps(scale_batch_fn sb, ncclComm_t c, int64_t dev_, int64_t W_, int G_)
         : scale_batch(sb), comm(c), dev(dev_), W(W_), G(G_),
           cs(comm_stream((c10::DeviceIndex)dev_)) {
         words = at::zeros({kSets * G, W}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
-        CBN_HIP_OK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        CBN_HIP_OK(hipEventCreateWithFlags(&tail, hipEventDisableTiming));
-        for (auto& e : set_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        CBN_HIP_OK(hipEventCreateWithFlags(&tail, kEvFlags));
+        for (auto& e : set_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, kEvFlags));
+        for (auto& e : ready_ev) CBN_HIP_OK(hipEventCreateWithFlags(&e, kEvFlags));
     }
     FoldHipOps(FoldHipOps&& o) noexcept
         : scale_batch(o.scale_batch), comm(o.comm), dev(o.dev), W(o.W), G(o.G), cs(o.cs), words(std::move(o.words)),
-          ready(o.ready), tail(o.tail) {
+          tail(o.tail) {
         for (int s = 0; s < kSets; ++s) {
             set_ev[s] = o.set_ev[s];
+            ready_ev[s] = o.ready_ev[s];
             set_used[s] = o.set_used[s];
-            o.set_ev[s] = nullptr;
+            o.set_ev[s] = o.ready_ev[s] = nullptr;
         }
-        o.ready = o.tail = nullptr;
+        o.tail = nullptr;
     }
     ~FoldHipOps() {
-        if (ready) (void)hipEventDestroy(ready);
         if (tail) (void)hipEventDestroy(tail);
         for (auto e : set_ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : ready_ev)
             if (e) (void)hipEventDestroy(e);
     }
     hipStream_t A() const { return c10::hip::getCurrentHIPStream(dev).stream(); }
@@ -759,10 +814,18 @@ struct FoldHipOps {
         CBN_HIP_OK(hipEventRecord(set_ev[set], on_comm ? cs.stream() : A()));
         set_used[set] = true;
     }
-    void handoff() {
-        CBN_HIP_OK(hipEventRecord(ready, A()));
-        CBN_HIP_OK(hipStreamWaitEvent(cs.stream(), ready, 0));
+    void record(int set) { CBN_HIP_OK(hipEventRecord(ready_ev[set], A())); }
+    bool passed(int set, bool block) {
+        if (block) {
+            CBN_HIP_OK(hipEventSynchronize(ready_ev[set]));
+            return true;
+        }
+        const hipError_t e = hipEventQuery(ready_ev[set]);
+        if (e == hipErrorNotReady) return false;
+        CBN_HIP_OK(e);
+        return true;
     }
+    void handoff(int set) { CBN_HIP_OK(hipStreamWaitEvent(cs.stream(), ready_ev[set], 0)); }
     int exchange(int set, int nb) {
         if (comm) {
             int* w = slot_words(set, 0);
@@ -802,7 +865,7 @@ class FoldStepper {
         : fold_(reinterpret_cast<fold_fn>(fold_addr)), plan_(reinterpret_cast<void*>(plan)), slots_(slots),
           first_(first), dev_(device_index), n_samples_(n_samples), target_observed_(target_observed),
           ring_(FoldHipOps(reinterpret_cast<scale_batch_fn>(scale_batch_addr), reinterpret_cast<ncclComm_t>(comm),
-                           device_index, n_words, group < 1 ? 1 : (group > 8 ? 8 : group)),
+                           device_index, n_words, group < 1 ? 1 : (group > kFoldGroupMax ? kFoldGroupMax : group)),
                 group) {}
 
     // this step's rows (final after wait()); None when a fast check failed (the
@@ -882,14 +945,16 @@ class FoldStepper {
 // ---- CPU test double of the folded ring: Python callbacks
 //   launch(set, index, payload, fold_payload or None, fold_set, fold_index) -> consumed (bool)
 //   exchange(set, n), scale([(payload, set, index), ...], on_comm), wait_set(set),
-//   mark_set(set, on_comm), handoff(), join()
+//   mark_set(set, on_comm), record(set), passed(set, block) -> bool, handoff(set), join()
 struct PyFoldOps {
     using Item = py::object;
     using P = FoldPending<py::object>;
     py::object cb;
     void wait_set(int set) { cb.attr("wait_set")(set); }
     void mark_set(int set, bool on_comm) { cb.attr("mark_set")(set, on_comm); }
-    void handoff() { cb.attr("handoff")(); }
+    void record(int set) { cb.attr("record")(set); }
+    bool passed(int set, bool block) { return cb.attr("passed")(set, block).cast<bool>(); }
+    void handoff(int set) { cb.attr("handoff")(set); }
     int exchange(int set, int nb) { return cb.attr("exchange")(set, nb).cast<int>(); }
     int scale(const std::vector<const P*>& run, bool on_comm) {
         py::list l;

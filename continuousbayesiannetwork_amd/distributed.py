@@ -240,7 +240,10 @@ class ShardedStepper:
         # max runs inside a later raw launch (cbn_plan_run_fold, FoldStepper)
         # instead of a separate scale launch
         self.fold = fold
-        self.G = max(1, min(8, exchange_every))
+        # steps per exchange group: <= 8 for the separate batched scale (one
+        # cbn_scale_batch per group), <= 32 when the scales are folded
+        self.G_req = max(1, exchange_every)
+        self.G = min(8, self.G_req)
         # force_exchange: all-reduce even at world size 1 (exercises RCCL on one GPU)
         multi = dist.is_initialized() and dist.get_world_size(group) > 1
         self.exchange = force_exchange or multi
@@ -283,6 +286,7 @@ class ShardedStepper:
         self._folded = (self.fold and not self.gather and int(fp.words.numel()) <= 256
                         and bool(lib.cbn_plan_flags(plan.handle) & _native.CBN_PLAN_STAGED))
         if self._folded:
+            self.G = min(32, self.G_req)
             self._c = host.FoldStepper(ctypes.cast(lib.cbn_plan_run_fold, ctypes.c_void_p).value, scale_batch,
                                        plan.handle.value, fp.slot_keys, fp.first, fp.device.index, plan.n_samples,
                                        plan.target_observed, int(fp.words.numel()), self.G, self._comm)

@@ -448,6 +448,8 @@ class _FoldOps:
         self.words = torch.zeros((3 * G, W), dtype=torch.int32)
         self.valid = [set(), set(), set()]  # exchanged words not yet consumed
         self.comm_pending = [False, False, False]  # a comm op on the set not yet waited by compute
+        self.rec = [None, None, None]  # a group's record on A: recorded -> passed / handed -> exchanged
+        self.queries = 0
         self.log = []
 
     def _div(self, item, s, i):
@@ -478,6 +480,8 @@ class _FoldOps:
         return consumed
 
     def exchange(self, s, nb):
+        assert self.rec[s] in ("passed", "handed"), ("exchange before A passed the group", s)
+        self.rec[s] = None
         grp = self.words[s * self.G: s * self.G + nb]
         dist.all_reduce(grp, op=dist.ReduceOp.MAX)
         self.valid[s] = set(range(nb))
@@ -499,8 +503,23 @@ class _FoldOps:
     def wait_set(self, s):
         self.comm_pending[s] = False
 
-    def handoff(self):
-        self.log.append(("handoff",))
+    def record(self, s):
+        assert self.rec[s] is None, ("record over a group not yet exchanged", s)
+        self.rec[s] = "recorded"
+
+    def passed(self, s, block):
+        # A passed the record: always when the host blocks, otherwise every other query
+        assert self.rec[s] == "recorded", ("query of a set with no record", s)
+        self.queries += 1
+        if block or self.queries % 2:
+            self.rec[s] = "passed"
+            return True
+        return False
+
+    def handoff(self, s):
+        assert self.rec[s] == "recorded", ("hand-off without a record", s)
+        self.rec[s] = "handed"
+        self.log.append(("handoff", s))
 
     def join(self):
         self.comm_pending = [False, False, False]

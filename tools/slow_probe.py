@@ -63,17 +63,26 @@ def blocker(n_blocks):
     return hook
 
 
-def stepper(comm, fold, n_block=0):
-    st = ShardedStepper(bn, "X19", 32, force_exchange=comm, exchange_every=8, fold=fold)
+def stepper(comm, fold, n_block=0, ring=0):
+    st = ShardedStepper(bn, "X19", 32, force_exchange=comm, exchange_every=int(os.environ.get("G", "8")), fold=fold)
     hook = blocker(n_block) if n_block else None
+    outs = [torch.empty((65536, 32), device=dev) for _ in range(ring)]
+    k = [0]
 
     def step(e):
-        st.step(e)
+        if ring:
+            k[0] += 1
+            st.step(e, out=outs[k[0] % ring])
+        else:
+            st.step(e)
         if hook:
             hook()
     rounds(f"stepper comm={comm} fold={fold} blocker={n_block}", step, st.wait)
     st.close()
 
+
+if os.environ.get("STREAM") == "1":  # a non-default current stream for everything
+    torch.cuda.set_stream(torch.cuda.Stream())
 
 for what in sys.argv[1:]:
     if what in ("pg_nccl", "pg_gloo"):  # a torch process group first, as bench.py has one
@@ -91,4 +100,5 @@ for what in sys.argv[1:]:
         rounds("fused", lambda e: bn.infer("X19", e, N_max=32))
     else:
         parts = what.split(",")
-        stepper(parts[0] == "comm", parts[1] == "fold", int(parts[2]) if len(parts) > 2 else 0)
+        stepper(parts[0] == "comm", parts[1] == "fold", int(parts[2]) if len(parts) > 2 else 0,
+                int(parts[3]) if len(parts) > 3 else 0)
