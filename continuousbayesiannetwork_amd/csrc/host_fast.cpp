@@ -592,7 +592,14 @@ int scale(uintptr_t fn, const at::Tensor& out, uintptr_t max_ptr, int32_t n_max)
 // every unfinished step on C, then joins.  FoldRing is that bookkeeping only;
 // FoldHipOps binds it to HIP / RCCL / cbn_plan_run_fold, PyFoldOps to Python
 // callbacks (the world-size-2 gloo test drives the same ring on CPU).
-constexpr int kSets = 3;
+#ifndef CBN_FOLD_SETS
+#define CBN_FOLD_SETS 3
+#endif
+constexpr int kSets = CBN_FOLD_SETS;
+// a group's steps are folded kFoldLag groups later.  Measured (NB=64,
+// profiles/r03_stepper_probe.txt): 4 sets (lag 3, rows 24-31 steps old) 11.9
+// vs 11.2 us per step for 3 -- the folded rows fall out of the MALL.
+constexpr int kFoldLag = kSets - 1;
 constexpr int kFoldGroupMax = 32;
 
 template <class Item>
@@ -675,7 +682,7 @@ class FoldRing {
         for (auto& grp : exch_) {
             if (grp.handed) continue;
             const int gset = (int)(grp.g % kSets);
-            const bool need = grp.g <= g_ - 2;
+            const bool need = grp.g <= g_ - kFoldLag;
             if (!ops_.passed(gset, /*block=*/need)) break;
             const int rc = hand(grp, /*eager=*/false);
             if (rc) return rc;
@@ -713,7 +720,7 @@ class FoldRing {
             if (rc) return rc;
         }
         // groups exchanged two or more groups back (handed above) become foldable
-        while (!exch_.empty() && exch_.front().g <= g_ - 2) {
+        while (!exch_.empty() && exch_.front().g <= g_ - kFoldLag) {
             Group& grp = exch_.front();
             if (!grp.items.empty()) ops_.wait_set(grp.items.front().set);  // their all-reduce done
             for (auto& p : grp.items) foldq_.push_back(std::move(p));
