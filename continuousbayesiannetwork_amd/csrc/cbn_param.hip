@@ -75,10 +75,30 @@ struct alignas(16) PRec {
 static_assert(sizeof(PRec) == 128, "PRec layout");
 constexpr int kRecFloats = sizeof(PRec) / 4;
 
+// Per-factor hot header (64 B, one scalar load) of the column-table kernels
+// whose factors all have every parent observed (M1): everything the factor
+// loop reads per factor, at an address known without a dependent load (the
+// header array follows the {0, 1} cell), so the next factor's header is in
+// flight while the current one is evaluated.
+struct alignas(16) PHead {
+    int kind;      // CBN_FACTOR_*
+    int row;       // image offset: node samples (QUERY) or the query-independent row
+    int wp;        // image offset: pair-packed MLP weights (n_layers 2) or [w0..w3, bias] (linear)
+    int n_in;
+    int hid;       // hidden width (n_layers 2)
+    int n_layers;
+    int act;
+    float scale;
+    float inv_scale;
+    float norm;
+    int pad[6];
+};
+static_assert(sizeof(PHead) == 64, "PHead layout");
+constexpr int kHeadFloats = sizeof(PHead) / 4;
+
 // Kernel-argument pointer table (3 KiB of the 4 KiB kernarg space).  Table
-// mode: p[f * kTabIn + i] = column of input i of factor f (evidence, or a
-// dummy column -- the output buffer, >= Q floats -- for inputs that are not
-// evidence: their loads are ignored), read with scalar loads into SGPRs.
+// mode: p[f * kTabIn + i] = column of input i of factor f (evidence, or null
+// for inputs that are not evidence: not loaded), read with scalar loads into SGPRs.
 // Slot mode (plans beyond the table): p[slot] = evidence column of the slot.
 constexpr int kTabIn = 4;
 constexpr int kTabCols = 384;  // 96 factors x 4 inputs
@@ -145,7 +165,7 @@ __device__ __forceinline__ f2 f2s(float a) { return f2{a, a}; }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // exp_split on a pair (the two v_exp_f32 are scalar: transcendentals do not pack)
-__device__ __forceinline__ f2 exp_split2(f2 x) {
+__device__ __forceinline__ f2 exp_split2_full(f2 x) {
 #pragma clang fp contract(off)
     constexpr float kL = 1.44269502162933349609375f;
     constexpr float kLlo = 1.925963033500e-8f;
@@ -161,6 +181,40 @@ __device__ __forceinline__ f2 exp_split2(f2 x) {
         r.x = ph.x < -126.f ? sx : r.x;
         r.y = ph.y < -126.f ? sy : r.y;
     }
+    return fma2(r, pl * f2s(kLn2), r);
+}
+
+// exp_split2 with the clamp and the subnormal fix-up taken only when some
+// lane of the wave needs them: where no lane has x log2(e) < -126 (so x >
+// -104 and the result is normal) the clamp is a no-op and the fix-up is
+// skipped by exp_split2_full too, so the bits are the same; otherwise the
+// whole wave runs exp_split2_full.  4 VALU slots fewer per pair.
+__device__ __forceinline__ f2 exp_split2(f2 x) {
+#pragma clang fp contract(off)
+    constexpr float kL = 1.44269502162933349609375f;
+    constexpr float kLlo = 1.925963033500e-8f;
+    constexpr float kLn2 = 0.693147180559945309f;
+    const f2 ph = x * f2s(kL);
+    if (__builtin_expect(__any(fminf(ph.x, ph.y) < -126.f), 0)) return exp_split2_full(x);
+    const f2 pl = fma2(x, f2s(kLlo), fma2(x, f2s(kL), -ph));
+    const f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
+    return fma2(r, pl * f2s(kLn2), r);
+}
+
+// exp(-0.5 t2) (the Gaussian's exp(-0.5 ((x - mu) / s)^2)) == exp_split2(-0.5f * t2)
+// bit for bit without the multiply: -0.5 t2 is exact (a power-of-two scale;
+// t2 >= 0, and where it would round, t2 < 2^-125, the result is 1 either
+// way), so x log2(e) = t2 (-0.5 log2(e)) and the residual fmas take the
+// halved constants exactly.
+__device__ __forceinline__ f2 exp_neg_half2(f2 t2) {
+#pragma clang fp contract(off)
+    constexpr float kHL = -0.5f * 1.44269502162933349609375f;
+    constexpr float kHLlo = -0.5f * 1.925963033500e-8f;
+    constexpr float kLn2 = 0.693147180559945309f;
+    const f2 ph = t2 * f2s(kHL);
+    if (__builtin_expect(__any(fminf(ph.x, ph.y) < -126.f), 0)) return exp_split2_full(f2s(-0.5f) * t2);
+    const f2 pl = fma2(t2, f2s(kHLlo), fma2(t2, f2s(kHL), -ph));
+    const f2 r = f2{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)};
     return fma2(r, pl * f2s(kLn2), r);
 }
 
@@ -505,7 +559,7 @@ template <int MODE>
 __device__ __forceinline__ f2 pdf2_t(float scale, float inv_scale, float norm, f2 x, float mu) {
     if (MODE <= 1) {
         const f2 t = MODE == 0 ? (x - f2s(mu)) : div_nr2(x - f2s(mu), f2s(scale), f2s(inv_scale));
-        return f2s(norm) * exp_split2(f2s(-0.5f) * (t * t));
+        return f2s(norm) * exp_neg_half2(t * t);
     }
     const f2 d = MODE == 2 ? (x - f2s(mu)) : div_nr2(x - f2s(mu), f2s(scale), f2s(inv_scale));
     const f2 e = exp_split2(-d);
@@ -588,6 +642,16 @@ __device__ __forceinline__ void mul_row(int mode, float (&acc)[NC], const float*
     }
 }
 
+// mu of a linear model with <= kTabIn inputs from its zero-padded weights
+// [w0..w3, bias]: the same fma chain as model_mu<0> (a padding term adds
+// fma(0, 0, s) == s), every weight an unconditional scalar load
+__device__ __forceinline__ float lin4(const float* __restrict__ LW, const float (&z)[kMaxP]) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kTabIn; ++i) s = fmaf(LW[i], z[i], s);  // z[i] = 0 beyond n_in (load_inputs_tab)
+    return s + LW[kTabIn];
+}
+
 // Column of one model input, resolved once per block into LDS: element
 // q of the input is p[q * stride] (stride 0: a constant / unused input reading
 // the image's {0, 1} cell).
@@ -607,9 +671,14 @@ __device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long
     }
 }
 
+// (table mode: a null column -- an input that is not evidence -- is not
+// loaded, a wave-uniform branch; its z is 0 until a free-parent combo sets it)
 __device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, long long qs, float (&z)[kMaxP]) {
 #pragma unroll
-    for (int i = 0; i < kTabIn; ++i) z[i] = gload(ev.p[f * kTabIn + i], qs);
+    for (int i = 0; i < kTabIn; ++i) {
+        const float* p = ev.p[f * kTabIn + i];
+        z[i] = p ? gload(p, qs) : 0.f;
+    }
 #pragma unroll
     for (int i = kTabIn; i < kMaxP; ++i) z[i] = 0.f;
 }
@@ -636,8 +705,24 @@ struct FSplit {
     int f[5];
 };
 
-template <int NC, int HMAX, int MODE, bool TAB>
+// Occupancy target per instantiation (waves per SIMD the register
+// allocation must allow).  The grid holds up to 8 waves per SIMD
+// (1 024 blocks x 8 waves); a linear-model wave's latency chain (scalar
+// weight / sample loads, the next factor's evidence) is only hidden with all
+// of them resident.
+#ifndef CBN_WPE_LIN
+#define CBN_WPE_LIN 8
+#endif
+#ifndef CBN_WPE_MLP
+#define CBN_WPE_MLP 1
+#endif
+// M1: every query factor of the plan has all its parents observed (M == 1,
+// e.g. full evidence): the free-combo mean and its TwoSum state (2 x NC
+// registers) are not compiled, which keeps the wave within the register
+// budget of the occupancy above.
+template <int NC, int HMAX, int MODE, bool TAB, bool M1>
 __global__ void __launch_bounds__(kQThreads)
+__attribute__((amdgpu_waves_per_eu(!M1 ? 1 : HMAX == 0 ? CBN_WPE_LIN : HMAX == 1 ? CBN_WPE_MLP : 1, 8)))
 k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
               int n_words, unsigned* __restrict__ max_out, float* __restrict__ out, FSplit sp) {
     const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);
@@ -684,6 +769,37 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
         if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qs, z);
         else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
+        if constexpr (M1 && TAB) {  // hot headers, one factor ahead
+            const PHead* __restrict__ hd = reinterpret_cast<const PHead*>(img + cst_off + 4);
+            PHead h = hd[fa < nf ? fa : nf - 1];
+            for (int f = fa; f < f1; ++f) {
+                float zn[kMaxP];
+                const int fn = f + 1 < f1 ? f + 1 : f;
+                load_inputs_tab(ev, fn, qs, zn);
+                const PHead hn = hd[fn];
+                const float* R = img + h.row + col0;
+                if (h.kind != CBN_FACTOR_QUERY) {
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * R[j];
+                } else {
+                    float mu;
+                    if (HMAX == 0 || h.n_layers == 1) {
+                        mu = lin4(img + h.wp, z);
+                    } else {
+                        const float* PW = img + h.wp;
+                        switch (h.act) {
+                            case CBN_ACT_TANH: mu = mlp1p_nin<CBN_ACT_TANH, kTabIn>(PW, h.n_in, h.hid, z, CBN_ACT_TANH); break;
+                            case CBN_ACT_RELU: mu = mlp1p_nin<CBN_ACT_RELU, kTabIn>(PW, h.n_in, h.hid, z, CBN_ACT_RELU); break;
+                            default: mu = mlp1p_rt(PW, h.n_in, h.hid, z, h.act); break;
+                        }
+                    }
+                    mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, R, h.scale, h.inv_scale, h.norm, mu);
+                }
+#pragma unroll
+                for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
+                h = hn;
+            }
+        } else
         for (int f = fa; f < f1; ++f) {
             const PRec& r = rec[f];
             float zn[kMaxP];
@@ -699,9 +815,9 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 const float* S = img + r.s_off + col0;
                 const int mode = mode_of(r.family, r.unit != 0);
                 const float sc = r.scale, isc = r.inv_scale, nm = r.norm;
-                if (r.M == 1) {  // every parent observed: x = pdf (a mean over size-1 axes)
+                if (M1 || r.M == 1) {  // every parent observed: x = pdf (a mean over size-1 axes)
                     mul_row<NC, MODE>(mode, acc, S, sc, isc, nm, query_mu<HMAX, kNMax>(r, img, W, z, deep));
-                } else {
+                } else if constexpr (!M1) {
                     float fx[NC], cx[NC];
 #pragma unroll
                     for (int j = 0; j < NC; ++j) fx[j] = cx[j] = 0.f;
@@ -1189,6 +1305,8 @@ struct ParamPlan {
     int mode = 4;    // density family of every query factor (0..3) or 4: mixed
     int cst_off = 0; // image offset of the {0, 1} cell read by constant inputs
     bool tab_ok = false;  // <= kTabIn inputs per factor and nf * kTabIn <= kTabCols: kernarg column table
+    bool all_m1 = false;  // every query factor has all its parents observed (M == 1): the M1 kernels
+    int parts = 1;        // factor ranges per query group (a plan constant: the product order)
     std::vector<int> in_slot;  // [nf][kTabIn] host copy (table mode)
     size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
     size_t deep_const = 0;  // ... and of the const kernel
@@ -1204,10 +1322,10 @@ struct ParamPlan {
 }  // namespace cbn
 
 namespace {
-template <int NC, int HMAX, int MODE, bool TAB = (MODE < 4)>
+template <int NC, int HMAX, int MODE, bool M1 = false, bool TAB = (MODE < 4)>
 void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
                     unsigned* words, float* out, hipStream_t s, int parts) {
-    allow_deep(&k_param_query<NC, HMAX, MODE, TAB>);
+    allow_deep(&k_param_query<NC, HMAX, MODE, TAB, M1>);
     FSplit sp;
     memset(&sp, 0, sizeof(sp));
     sp.parts = parts;
@@ -1216,7 +1334,7 @@ void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long
     lds = (lds + 15) & ~(size_t)15;
     sp.comb_off = (int)(lds / sizeof(float));
     if (parts > 1) lds += (size_t)(kQThreads / kWave) * NC * kWave * sizeof(float);
-    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
+    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB, M1>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
                        pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out, sp);
 }
 
@@ -1226,17 +1344,30 @@ void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long
 bool specialised(int hmax, int mode) { return mode < 4 && (hmax == 0 || mode >= 2); }
 
 // MLP (NeuralNetwork, logistic density) kernels for one column chunk
+// (one-hidden-layer plans with every parent observed: the M1 forms)
 template <int NC>
 void launch_query_mlp(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
                       unsigned* words, float* out, hipStream_t s, int parts) {
-#define CBN_Q(H, M) launch_query_t<NC, H, M>(pp, grid, ev, Q, QW, L, words, out, s, parts)
+#define CBN_Q(H, M, M1) launch_query_t<NC, H, M, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts)
     switch (pp->hmax * 8 + pp->mode) {
-        case 1 * 8 + 2: CBN_Q(1, 2); break;
-        case 1 * 8 + 3: CBN_Q(1, 3); break;
-        case 32 * 8 + 2: CBN_Q(32, 2); break;
-        default: CBN_Q(32, 3); break;
+        case 1 * 8 + 2: if (pp->all_m1) CBN_Q(1, 2, true); else CBN_Q(1, 2, false); break;
+        case 1 * 8 + 3: if (pp->all_m1) CBN_Q(1, 3, true); else CBN_Q(1, 3, false); break;
+        case 32 * 8 + 2: CBN_Q(32, 2, false); break;
+        default: CBN_Q(32, 3, false); break;
     }
 #undef CBN_Q
+}
+
+// linear models (LinearRegression / LogisticRegression): 8-column chunks
+template <bool M1>
+void launch_query_lin(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
+                      unsigned* words, float* out, hipStream_t s, int parts) {
+    switch (pp->mode) {
+        case 0: launch_query_t<8, 0, 0, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        case 1: launch_query_t<8, 0, 1, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        case 2: launch_query_t<8, 0, 2, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        default: launch_query_t<8, 0, 3, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+    }
 }
 }  // namespace
 
@@ -1263,7 +1394,7 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     if (specialised(pp->hmax, pp->mode)) {  // table mode: one pointer per (factor, input)
         for (size_t e = 0; e < pp->in_slot.size(); ++e) {
             const int sl = pp->in_slot[e];
-            ev.p[e] = sl >= 0 ? evidence[sl] : out;  // dummy column (>= Q floats), value unused
+            ev.p[e] = sl >= 0 ? evidence[sl] : nullptr;  // not evidence: not loaded (z = 0 / a free combo's sample)
         }
     } else {
         for (int i = 0; i < n_evidence; ++i) ev.p[i] = evidence[i];
@@ -1293,12 +1424,8 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     const int L = (pp->N + nc - 1) / nc;
     const long long waves = QW * L;
     if (waves >= (1LL << 31)) return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
-    // factor split: a plan constant (never a function of the batch size), so
-    // the product order -- and every row bit -- is the same however the batch
-    // is sharded.  Two parts: configs[3] NN [16] at 131 072 queries 304 -> 218
-    // us, LR and 1 M-query batches unchanged within noise (4 parts: 215 us at
-    // 131 072, 2 % slower at 1 M), profiles/r01_bench_cont.json.
-    int parts = pp->nf >= 2 ? 2 : 1;
+    // factor split (ParamPlan::parts; CBN_PARAM_PARTS overrides it for A/B)
+    int parts = pp->parts;
     if (const char* e = getenv("CBN_PARAM_PARTS")) {
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) parts = v;
@@ -1310,12 +1437,8 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     if (!specialised(pp->hmax, pp->mode)) {
         launch_query_t<16, 32, 4>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
     } else if (pp->hmax == 0) {  // linear models: 8-column chunks
-        switch (pp->mode) {
-            case 0: launch_query_t<8, 0, 0>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
-            case 1: launch_query_t<8, 0, 1>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
-            case 2: launch_query_t<8, 0, 2>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
-            default: launch_query_t<8, 0, 3>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
-        }
+        if (pp->all_m1) launch_query_lin<true>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
+        else launch_query_lin<false>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
     } else {
         switch (nc) {
             case 8: launch_query_mlp<8>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
@@ -1478,7 +1601,8 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     std::vector<PRec> recs(n_factors);
     std::vector<int> consts;
     const long long cst_off = (long long)n_factors * kRecFloats;  // {0, 1}: constant model inputs
-    long long off = cst_off + 4;
+    long long off = cst_off + 4 + (long long)n_factors * kHeadFloats;  // then the PHead array
+    std::vector<int> lw_off(n_factors, 0);  // linear models with <= kTabIn inputs: [w0..w3, bias] copy
     int ns = 0, hmax = 0;
     for (int f = 0; f < n_factors; ++f) {
         const cbn_param_factor& h = factors[f];
@@ -1527,6 +1651,9 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             const long long npairs = (r.m.width[1] + 1) / 2;
             r.pw_off = (int)off;
             off += (npairs * (2LL * r.m.width[0] + 4) + 1 + 3) & ~3LL;
+        } else if (r.m.n_layers == 1 && r.m.width[0] <= kTabIn) {
+            lw_off[f] = (int)off;
+            off += 8;
         }
         const long long row = (N + kColPad - 1) / kColPad * kColPad;  // padded: chunk reads never leave the row
         r.s_off = (int)off;
@@ -1558,6 +1685,16 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         pp->mode = pp->mode < 0 || pp->mode == m ? m : 4;
     }
     if (pp->mode < 0) pp->mode = 0;  // no query factor
+    pp->all_m1 = !getenv("CBN_PARAM_NO_M1");
+    for (const PRec& r : recs) pp->all_m1 = pp->all_m1 && (r.kind != CBN_FACTOR_QUERY || r.M == 1);
+    // factor split: a plan constant (never a function of the batch size), so
+    // the product order -- and every row bit -- is the same however the batch
+    // is sharded.  Two parts by default (configs[3] NN [16] at 131 072
+    // queries 304 -> 218 us in round 1, profiles/r01_bench_cont.json); four
+    // for one-hidden-layer M1 plans, whose kernel holds 6 waves per SIMD
+    // (NN [16] at 131 072 queries 136 -> 125 us, 1 M queries +3 %).
+    pp->parts = n_factors >= 2 ? 2 : 1;
+    if (pp->all_m1 && hmax == 1 && n_factors >= 8) pp->parts = 4;
     pp->image_floats = (int)off;
     pp->cst_off = (int)cst_off;
     pp->tab_ok = (long long)n_factors * kTabIn <= kTabCols;
@@ -1648,6 +1785,34 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             ok = ok && hipMemcpy(pp->d_image + r.pw_off, pw.data(), sizeof(float) * pw.size(), hipMemcpyHostToDevice) ==
                            hipSuccess;
         }
+        if (ok && lw_off[f]) {  // zero-padded linear weights: [w0..w_{n-1}, 0.., bias at kTabIn]
+            const int n = r.m.width[0];
+            std::vector<float> w(n + 1), lw(8, 0.f);
+            ok = hipMemcpy(w.data(), h.model.weights, sizeof(float) * (n + 1), hipMemcpyDeviceToHost) == hipSuccess;
+            for (int i = 0; i < n; ++i) lw[i] = w[i];
+            lw[kTabIn] = w[n];
+            ok = ok && hipMemcpy(pp->d_image + lw_off[f], lw.data(), sizeof(float) * 8, hipMemcpyHostToDevice) == hipSuccess;
+        }
+    }
+    if (ok) {  // hot headers (PHead) of the M1 column-table kernels
+        std::vector<PHead> heads(n_factors);
+        for (int f = 0; f < n_factors; ++f) {
+            const PRec& r = recs[f];
+            PHead& hh = heads[f];
+            memset(&hh, 0, sizeof(hh));
+            hh.kind = r.kind;
+            hh.row = r.kind == CBN_FACTOR_QUERY ? r.s_off : r.c_off;
+            hh.wp = r.m.n_layers == 2 ? r.pw_off : lw_off[f];
+            hh.n_in = r.m.width[0];
+            hh.hid = r.m.n_layers == 2 ? r.m.width[1] : 0;
+            hh.n_layers = r.m.n_layers;
+            hh.act = r.m.act;
+            hh.scale = r.scale;
+            hh.inv_scale = r.inv_scale;
+            hh.norm = r.norm;
+        }
+        ok = hipMemcpy(pp->d_image + cst_off + 4, heads.data(), sizeof(PHead) * n_factors, hipMemcpyHostToDevice) ==
+             hipSuccess;
     }
     ok = ok && hipDeviceSynchronize() == hipSuccess;
     if (ok && !consts.empty()) {
