@@ -108,6 +108,12 @@ struct PEv {
 
 typedef const __attribute__((address_space(1))) float gfloat_t;
 __device__ __forceinline__ float gload(const float* p, long long i) { return ((gfloat_t*)p)[i]; }
+// element at a 32-bit byte offset: a uniform base plus one VGPR offset shared
+// by every column (global_load ... saddr), not a 64-bit address per column
+__device__ __forceinline__ float gload_b(const float* p, unsigned byte_off) {
+    typedef const __attribute__((address_space(1))) char gchar_t;
+    return *(gfloat_t*)((gchar_t*)p + byte_off);
+}
 
 __device__ __forceinline__ unsigned wave_max_u(unsigned v) {
 #pragma unroll
@@ -673,12 +679,13 @@ __device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long
 
 // (table mode: a null column -- an input that is not evidence -- is not
 // loaded, a wave-uniform branch; its z is 0 until a free-parent combo sets it)
-__device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, long long qs, float (&z)[kMaxP]) {
+struct alignas(16) PEv4 {
+    const float* p[kTabIn];
+};
+__device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, unsigned qb, float (&z)[kMaxP]) {
+    const PEv4 c = reinterpret_cast<const PEv4*>(ev.p)[f];  // the factor's column pointers: one scalar load
 #pragma unroll
-    for (int i = 0; i < kTabIn; ++i) {
-        const float* p = ev.p[f * kTabIn + i];
-        z[i] = p ? gload(p, qs) : 0.f;
-    }
+    for (int i = 0; i < kTabIn; ++i) z[i] = c.p[i] ? gload_b(c.p[i], qb) : 0.f;
 #pragma unroll
     for (int i = kTabIn; i < kMaxP; ++i) z[i] = 0.f;
 }
@@ -760,6 +767,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         const long long q = (long long)(t - l * QW) * kWave + lane;
         const bool valid = q < Q;
         const long long qs = valid ? q : Q - 1;
+        const unsigned qb = (unsigned)qs * 4u;  // table mode: Q <= 2^30 (param_run)
         const int col0 = l * NC;
         const int ncol = min(NC, N - col0);
         float acc[NC];
@@ -767,7 +775,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
         const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
-        if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qs, z);
+        if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qb, z);
         else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
         if constexpr (M1 && TAB) {  // hot headers, one factor ahead
             const PHead* __restrict__ hd = reinterpret_cast<const PHead*>(img + cst_off + 4);
@@ -775,7 +783,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             for (int f = fa; f < f1; ++f) {
                 float zn[kMaxP];
                 const int fn = f + 1 < f1 ? f + 1 : f;
-                load_inputs_tab(ev, fn, qs, zn);
+                load_inputs_tab(ev, fn, qb, zn);
                 const PHead hn = hd[fn];
                 const float* R = img + h.row + col0;
                 if (h.kind != CBN_FACTOR_QUERY) {
@@ -804,7 +812,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             const PRec& r = rec[f];
             float zn[kMaxP];
             const int fn = f + 1 < f1 ? f + 1 : f;  // next factor's evidence in flight during this one
-            if (TAB) load_inputs_tab(ev, fn, qs, zn);
+            if (TAB) load_inputs_tab(ev, fn, qb, zn);
             else load_inputs(incol + fn * kMaxP, qs, zn);
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
                 const float* c = img + r.c_off + col0;
@@ -1307,6 +1315,7 @@ struct ParamPlan {
     bool tab_ok = false;  // <= kTabIn inputs per factor and nf * kTabIn <= kTabCols: kernarg column table
     bool all_m1 = false;  // every query factor has all its parents observed (M == 1): the M1 kernels
     int parts = 1;        // factor ranges per query group (a plan constant: the product order)
+    bool lin16 = false;   // linear M1 plan with N >= 16: 16-column chunks (mu once per 16 columns)
     std::vector<int> in_slot;  // [nf][kTabIn] host copy (table mode)
     size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
     size_t deep_const = 0;  // ... and of the const kernel
@@ -1358,15 +1367,15 @@ void launch_query_mlp(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, lo
 #undef CBN_Q
 }
 
-// linear models (LinearRegression / LogisticRegression): 8-column chunks
-template <bool M1>
+// linear models (LinearRegression / LogisticRegression): NCL-column chunks
+template <int NCL, bool M1>
 void launch_query_lin(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long long Q, int QW, int L,
                       unsigned* words, float* out, hipStream_t s, int parts) {
     switch (pp->mode) {
-        case 0: launch_query_t<8, 0, 0, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
-        case 1: launch_query_t<8, 0, 1, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
-        case 2: launch_query_t<8, 0, 2, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
-        default: launch_query_t<8, 0, 3, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        case 0: launch_query_t<NCL, 0, 0, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        case 1: launch_query_t<NCL, 0, 1, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        case 2: launch_query_t<NCL, 0, 2, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
+        default: launch_query_t<NCL, 0, 3, M1>(pp, grid, ev, Q, QW, L, words, out, s, parts); break;
     }
 }
 }  // namespace
@@ -1420,10 +1429,12 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     // (<= 64 VGPRs: 8 waves per SIMD); MLPs keep whole rows up to 32 columns
     // (every extra chunk re-evaluates the network)
     int nc = pp->nc;
-    if (pp->hmax == 0 && specialised(pp->hmax, pp->mode)) nc = 8;
+    const bool lin16 = pp->lin16 && !getenv("CBN_PARAM_LIN8");
+    if (pp->hmax == 0 && specialised(pp->hmax, pp->mode)) nc = lin16 ? 16 : 8;
     const int L = (pp->N + nc - 1) / nc;
     const long long waves = QW * L;
-    if (waves >= (1LL << 31)) return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
+    if (waves >= (1LL << 31) || n_queries > (1LL << 30))
+        return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
     // factor split (ParamPlan::parts; CBN_PARAM_PARTS overrides it for A/B)
     int parts = pp->parts;
     if (const char* e = getenv("CBN_PARAM_PARTS")) {
@@ -1437,8 +1448,9 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     if (!specialised(pp->hmax, pp->mode)) {
         launch_query_t<16, 32, 4>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
     } else if (pp->hmax == 0) {  // linear models: 8-column chunks
-        if (pp->all_m1) launch_query_lin<true>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
-        else launch_query_lin<false>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
+        if (lin16) launch_query_lin<16, true>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
+        else if (pp->all_m1) launch_query_lin<8, true>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
+        else launch_query_lin<8, false>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts);
     } else {
         switch (nc) {
             case 8: launch_query_mlp<8>(pp, (unsigned)grid, ev, n_queries, (int)QW, L, words, out, s, parts); break;
@@ -1693,8 +1705,12 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     // queries 304 -> 218 us in round 1, profiles/r01_bench_cont.json); four
     // for one-hidden-layer M1 plans, whose kernel holds 6 waves per SIMD
     // (NN [16] at 131 072 queries 136 -> 125 us, 1 M queries +3 %).
+    // Linear M1 plans with N >= 16 take 16-column chunks and four parts
+    // (half the evidence loads and model evaluations of 8-column chunks at the
+    // same 8 waves per SIMD): LR at 131 072 queries 54 -> 48 us, 1 M 377 -> 331 us.
     pp->parts = n_factors >= 2 ? 2 : 1;
-    if (pp->all_m1 && hmax == 1 && n_factors >= 8) pp->parts = 4;
+    pp->lin16 = pp->all_m1 && hmax == 0 && N >= 16;
+    if (pp->all_m1 && (hmax == 1 || pp->lin16) && n_factors >= 8) pp->parts = 4;
     pp->image_floats = (int)off;
     pp->cst_off = (int)cst_off;
     pp->tab_ok = (long long)n_factors * kTabIn <= kTabCols;
