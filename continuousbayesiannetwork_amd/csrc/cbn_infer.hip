@@ -699,12 +699,15 @@ __global__ void __launch_bounds__(kQueryThreads)
 k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats, FPtrsT<NP> fp,
              long long Q, long long per, int N, int RS, int L, int paired, unsigned* __restrict__ sync,
              unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
-             float* __restrict__ out) {
+             float* __restrict__ out, int lds_tab, unsigned long long lmask0, unsigned long long lmask1) {
     CBN_STAMP_INIT;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
     const int nf4 = (nf + 3) & ~3;
-    const float** ptab = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : 0));  // [nf4][4]
+    // global-table plans: the small tables (image floats [0, lds_tab), factors
+    // in lmask) are copied to LDS; the others are gathered from L2 / MALL
+    if (USE_LDS) lds_tab = 0;
+    const float** ptab = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : lds_tab));  // [nf4][4]
     int* woffs_all = reinterpret_cast<int*>(ptab + NP);  // per wave: (64 / L) queries x nf4
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
@@ -719,6 +722,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const long long q1 = q0 + per < Q ? q0 + per : Q;
     const long long i_end = q1 * L;
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
+    else if (lds_tab > 0) lds_dma_copy(gimage, smem4, lds_tab / 4);  // the small tables
     if (tid < NP) ptab[tid] = fp.p[tid];
     (void)ns;
     CBN_STAMP(1);
@@ -858,10 +862,19 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 #pragma unroll
                 for (int k = 0; k < KB; ++k) {
                     const int o = oo[k];
-                    const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+                    const int fk = f0 + k;  // wave-uniform: is this factor's table in LDS?
+                    const bool in_lds = fk < nf && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0);
+                    if (in_lds) {
 #pragma unroll
-                    for (int v = 0; v < VPL; ++v)
-                        t[k][v] = (f0 + k < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        for (int v = 0; v < VPL; ++v)
+                            t[k][v] = o >= 0 ? reinterpret_cast<const float4*>(simg + (o < 0 ? 0 : o))[l * VPL + v]
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                    } else {
+                        const float4* row = reinterpret_cast<const float4*>(img + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+                        for (int v = 0; v < VPL; ++v)
+                            t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < KB; ++k) {
@@ -1583,7 +1596,7 @@ void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvP
     hipLaunchKernelGGL((k_query_fast<VPL, LDS, MODE, NP>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
                        p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, fast_ptrs<NP>(p, ev), Q,
                        (Q + blocks - 1) / blocks, p->N, p->RS, L, p->paired ? 1 : 0, p->d_sync, epoch, max_in, n_max,
-                       max_out, out);
+                       max_out, out, p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
 }
 
 template <int VPL, bool LDS, int MODE>
@@ -1885,12 +1898,55 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     }
     const int RS = paired ? 64 : vec == 4 && !global_tables ? N + 4 : N;
     const long long talign = global_tables ? 32 : 4;
+    // Global-table plans: the smallest tables go first in the image, as many as
+    // fit the LDS the fast kernel leaves free (without costing it its second
+    // block per CU), and k_query_fast copies that prefix into LDS -- an
+    // ALARM-like plan is 24 tables of <= 2 KB beside two of 128 KB, and
+    // gathering the small ones from L2 cost as much as the large ones.
+    std::vector<long long> pre_off(n_factors, -1);
+    long long lds_tab_end = 0;
+    unsigned long long lds_mask[2] = {0, 0};
+    if (global_tables && vec == 4 && n_factors <= 128 && !getenv("CBN_NO_LDS_SPLIT")) {
+        int vp = 0, Lp = 0;
+        for (int c : {2, 1}) {  // the fast path's choice (below)
+            if (c > want_vpl || (N / 4) % c) continue;
+            const int Lc = N / (4 * c);
+            if (Lc <= kWave && (kWave % Lc) == 0) { vp = c; Lp = Lc; break; }
+        }
+        if (vp > 0) {
+            const long long nf4 = (n_factors + 3) & ~3;
+            const long long side = (long long)kFastPtrs * sizeof(void*) +
+                                   (long long)(kQueryThreads / kWave) * (kWave / Lp) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
+            long long budget = (long long)kLdsBudget - side - 1024;  // bytes
+            if (2 * side <= (long long)kLdsBudget) budget = std::min(budget, (long long)kLdsBudget / 2 - side - 1024);
+            std::vector<std::pair<long long, int>> by_size;
+            for (int f = 0; f < n_factors; ++f) {
+                long long rows = 1;
+                for (int q = 0; q < factors[f].n_parents && q < kMaxP; ++q)
+                    if (factors[f].parent_ev_slot[q] >= 0 && factors[f].parent_card[q] > 0)
+                        rows = std::min(rows * factors[f].parent_card[q], 1LL << 40);
+                by_size.push_back({(rows * RS + talign - 1) & ~(talign - 1), f});
+            }
+            std::stable_sort(by_size.begin(), by_size.end());
+            for (const auto& [tf, f] : by_size) {
+                if ((lds_tab_end + tf) * 4 > budget) break;  // floats vs bytes
+                pre_off[f] = lds_tab_end;
+                lds_tab_end += tf;
+                lds_mask[f >> 6] |= 1ull << (f & 63);
+            }
+            if (lds_tab_end == 0 || lds_tab_end * 4 > (1LL << 20)) {
+                std::fill(pre_off.begin(), pre_off.end(), -1);
+                lds_tab_end = 0;
+                lds_mask[0] = lds_mask[1] = 0;
+            }
+        }
+    }
     long long class_start[2] = {0, 0};
     std::vector<DevFactor> fac(n_factors);
     std::vector<const float*> slot_dom(CBN_MAX_EVIDENCE, nullptr);
     std::vector<int> slot_card(CBN_MAX_EVIDENCE, 0);
     int ns = 0;
-    long long off = 0;
+    long long off = lds_tab_end;  // after the LDS-copied small tables (global-table plans)
     for (int f = 0; f < n_factors; ++f) {
         const cbn_factor_desc& h = factors[f];
         DevFactor& d = fac[f];
@@ -1950,6 +2006,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             d.table_off = (int)(class_start[c] * 64 + c * 32);
             class_start[c] += rows;
             off = std::max(class_start[0], class_start[1]) * 64;
+        } else if (pre_off[f] >= 0) {
+            if (pre_off[f] + rows * RS > lds_tab_end) return set_err(CBN_E_ARG, "factor %d: table size changed", f);
+            d.table_off = (int)pre_off[f];
         } else {
             d.table_off = (int)off;
             off += (rows * RS + talign - 1) & ~(talign - 1);
@@ -1993,6 +2052,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     P->prefix_rows = prefix > 0 ? fac[prefix].rows : 0;
     P->rec_off = (int)rec_off;
     P->RS = RS;
+    P->lds_tab_floats = (int)lds_tab_end;
+    P->lds_tab_mask[0] = lds_mask[0];
+    P->lds_tab_mask[1] = lds_mask[1];
     // LDS: [image (if staged)] [factor records] [slots] [CH x (ns + nf) ints] [wave maxima]
     const size_t fixed = (size_t)n_factors * kFqInts * 4 + (size_t)ns * sizeof(QSlot) + (kQueryThreads / kWave) * 4 +
                          (size_t)CBN_MAX_EVIDENCE * sizeof(void*) + 64;
@@ -2114,7 +2176,12 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                                        reinterpret_cast<const void*>(&k_query_staged<kModeRaw>)})
                     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
             }
-            P->fast_lds_bytes = ((P->use_lds ? img_bytes : 0) + side + 15) & ~size_t(15);
+            P->fast_lds_bytes = ((P->use_lds ? img_bytes : (size_t)P->lds_tab_floats * 4) + side + 15) & ~size_t(15);
+            if (P->fast_lds_bytes > (size_t)kLdsBudget) {  // the LDS-table prefix was sized for this side buffer
+                const size_t b = P->fast_lds_bytes;
+                cbn_plan_destroy(P);
+                return set_err(CBN_E_HIP, "cbn_plan_create: internal error, fast-path LDS %zu B", b);
+            }
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
             P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=

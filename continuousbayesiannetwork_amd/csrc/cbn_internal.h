@@ -92,6 +92,8 @@ struct cbn_plan {
     unsigned fused_epoch = 0;    // tag of the published {epoch, max} granule
     bool fused_ok = false;       // one block per CU fits (LDS/VGPR) -> grid barrier is safe
     size_t fast_lds_bytes = 0;
+    int lds_tab_floats = 0;      // global-table plans: the small tables packed first, copied to LDS by k_query_fast
+    unsigned long long lds_tab_mask[2] = {0, 0};  // ... and which factors' tables those are (bit f)
     int fast_blocks_per_cu = 1;
     int max_slots = 0;           // fast max/raw passes: blocks per launch at most = words of per-block maxima
     int image_floats = 0;
