@@ -9,8 +9,8 @@ script=$1; shift
 for round in 1 2; do
 for spec in "$@"; do
   IFS=: read -r name envs <<< "$spec"
-  env $envs timeout -k 10 300 python "$script" > gpurun_out/abe_$name.log 2>&1 || exit $?
+  env $envs timeout -k 10 300 python "$script" > gpurun_out/abe_$(basename $script .py)_$name.log 2>&1 || exit $?
   echo "== $name (round $round)"
-  grep '^{' gpurun_out/abe_$name.log | cut -c1-200
+  grep '^{' gpurun_out/abe_$(basename $script .py)_$name.log | cut -c1-200
 done
 done
