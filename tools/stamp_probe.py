@@ -15,18 +15,25 @@ lib = nat.load()
 lib.cbn_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
 S = 12
 buf = torch.zeros(4096 * 16 * S, dtype=torch.int64, device=dev)
-data, cols, edges = chain_data(20, 32, 200000, 3, stay=0.8)
+if os.environ.get("ALARM"):  # BASELINE configs[2]: k_query_fast on global tables (tools/bench_alarm.py)
+    from helpers import alarm_like_data
+    data, cols, edges = alarm_like_data(200_000, 5)
+    target, Q, NM = "X35", 262144, 8
+else:  # configs[1]: the staged kernel
+    data, cols, edges = chain_data(20, 32, 200000, 3, stay=0.8)
+    target, Q, NM = "X19", 65536, 32
 bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
 bn.engine.fused = os.environ.get("TWO_PASS") is None
+names_ev = [c for c in cols if c != target]
 evs = []
 for b in range(8):
-    evs.append({k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, cols[:-1], 65536, 1000 + b).items()})
+    evs.append({k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names_ev, Q, 1000 + b).items()})
 for i in range(40):
-    bn.infer("X19", evs[i % 8], N_max=32)
+    bn.infer(target, evs[i % 8], N_max=NM)
 torch.cuda.synchronize()
 nat.check(lib.cbn_debug_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())), "stamps")
 buf.zero_()
-bn.infer("X19", evs[3], N_max=32)
+bn.infer(target, evs[3], N_max=NM)
 torch.cuda.synchronize()
 st = buf.view(-1, S).cpu().numpy()
 st = st[st[:, 0] > 0]
