@@ -706,8 +706,11 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const int nf4 = (nf + 3) & ~3;
     // global-table plans: the small tables (image floats [0, lds_tab), factors
     // in lmask) are copied to LDS; the others are gathered from L2 / MALL
+    // (and the factor records follow them in LDS: the index loop's record reads
+    // are then LDS reads, which do not wait behind the evidence loads in flight)
     if (USE_LDS) lds_tab = 0;
-    const float** ptab = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : lds_tab));  // [nf4][4]
+    const float** ptab =
+        reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : lds_tab + nf * kRecFloats));  // [nf4][4]
     int* woffs_all = reinterpret_cast<int*>(ptab + NP);  // per wave: (64 / L) queries x nf4
     const int tid = threadIdx.x;
     const int nthr = blockDim.x;
@@ -722,14 +725,18 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const long long q1 = q0 + per < Q ? q0 + per : Q;
     const long long i_end = q1 * L;
     if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);  // tables + domains + records
-    else if (lds_tab > 0) lds_dma_copy(gimage, smem4, lds_tab / 4);  // the small tables
+    else {
+        if (lds_tab > 0) lds_dma_copy(gimage, smem4, lds_tab / 4);  // the small tables
+        lds_dma_copy(gimage + rec_off, smem4 + lds_tab / 4, nf * kRecFloats / 4);  // the records
+    }
     if (tid < NP) ptab[tid] = fp.p[tid];
     (void)ns;
     CBN_STAMP(1);
     __syncthreads();  // LDS image (waits vmcnt(0)) + evidence column pointers ready
     CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
-    const FastRec* rec = reinterpret_cast<const FastRec*>(img + rec_off);
+    const FastRec* rec = reinterpret_cast<const FastRec*>(USE_LDS ? simg + rec_off : simg + lds_tab);
+    const int lsh = __builtin_ctz(L);  // L: a power of two (query index = item >> lsh)
 
     float maxv = 1.f;
     if (MODE == kModeWrite) {
@@ -764,51 +771,47 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     long long fq = -1;  // fused: the one query this lane holds (-1: none)
     // wave-uniform round loop: a wave's 64 items are qpw whole queries
     float x[kLoc][kFastObs];
-    // evidence of round wb into x: first observed parent of each of the lane's
-    // factors -- all pointer reads, then all loads (unbranched: entry f*4 is
-    // never null) -- then the rare further parents
-    // factors are taken in chunks of kLoc*L (one chunk unless nf > 8 L)
-    auto load_x = [&](long long wb, int c0) {
-        const long long q = wb + lane < i_end ? (wb + lane) / L : q0;
-        uintptr_t p0[kLoc];
+    // Evidence of slot j of chunk c0 of round wb into x[j]: every observed
+    // parent of the lane's factor c0 + l + j L, always kFastObs loads (an absent
+    // parent reads row 0 of the first column), so the number of loads in flight
+    // is static and the compiler's waits count them.  The factors are taken in
+    // chunks of kLoc * L, and slot j is refilled with the NEXT chunk's (or the
+    // next round's first chunk's) evidence as soon as its domain index is done:
+    // the evidence loads of a chunk fly while the previous chunk is indexed,
+    // instead of one memory round trip per chunk.
+    auto q_of = [&](long long wb) { return wb + lane < i_end ? (wb + lane) >> lsh : q0; };
+    auto load_one = [&](long long q, int c0, int j) {
+        const int f = c0 + l + j * L;
+        const int fs = f < nf ? f : 0;
+        const uintptr_t p0 = reinterpret_cast<uintptr_t>(ptab[fs * kFastObs]);
+        const float* col = reinterpret_cast<const float*>(p0 & ~(kTagMore | kTagNone));
+        x[j][0] = gload(col, (p0 & kTagNone) ? 0 : q);
 #pragma unroll
-        for (int j = 0; j < kLoc; ++j) {
-            const int f = c0 + l + j * L;
-            p0[j] = reinterpret_cast<uintptr_t>(ptab[(f < nf ? f : 0) * kFastObs]);
-        }
-#pragma unroll
-        for (int j = 0; j < kLoc; ++j) {
-            const float* col = reinterpret_cast<const float*>(p0[j] & ~(kTagMore | kTagNone));
-            x[j][0] = gload(col, (p0[j] & kTagNone) ? 0 : q);
-        }
-#pragma unroll
-        for (int j = 0; j < kLoc; ++j) {
-            const int f = c0 + l + j * L;
-            if (f < nf && (p0[j] & kTagMore)) {  // rare: factors with several observed parents
-#pragma unroll
-                for (int p = 1; p < kFastObs; ++p) {
-                    const float* col = ptab[f * kFastObs + p];
-                    if (col) x[j][p] = gload(col, q);
-                }
-            }
+        for (int p = 1; p < kFastObs; ++p) {
+            const float* cp = (f < nf && (p0 & kTagMore)) ? ptab[fs * kFastObs + p] : nullptr;
+            x[j][p] = gload(cp ? cp : col, cp ? q : 0);
         }
 #ifdef CBN_CHECKED
-        if (!CBN_OK_OR(q >= 0 && q < Q, 2)) {
-#pragma unroll
-            for (int j = 0; j < kLoc; ++j) x[j][0] = -1.f;
-        }
+        if (!CBN_OK_OR(q >= 0 && q < Q, 2)) x[j][0] = -1.f;
 #endif
     };
     long long wbase = q0 * L + (long long)wid * kWave;
-    if (wbase < i_end) load_x(wbase, 0);
+    if (wbase < i_end) {
+        const long long qf = q_of(wbase);
+#pragma unroll
+        for (int j = 0; j < kLoc; ++j) load_one(qf, 0, j);
+    }
     const int chunk = kLoc * L;
     for (; wbase < i_end; wbase += nthr) {
         const long long it = wbase + lane;
         const bool valid = it < i_end;
-        const long long q = valid ? it / L : q0;
+        const long long q = valid ? it >> lsh : q0;
         if (first) CBN_STAMP(3);
         for (int c0 = 0; c0 < nf; c0 += chunk) {  // wave-uniform
-        if (c0 > 0) load_x(wbase, c0);
+        const bool more = c0 + chunk < nf;  // refill target: this round's next chunk, else the next round's first
+        const bool refill = more || wbase + nthr < i_end;
+        const long long qn = q_of(more ? wbase : wbase + nthr);
+        const int cn = more ? c0 + chunk : 0;
 #pragma unroll
         for (int j = 0; j < kLoc; ++j) {
             const int f = c0 + l + j * L;
@@ -838,6 +841,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 }
                 my[f] = o;
             }
+            if (refill) load_one(qn, cn, j);  // x[j] is consumed
         }
         }  // chunks
         // the offsets of this query were written by lanes of this same wave:
@@ -845,8 +849,7 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
         if (first) CBN_STAMP(4);
-        // x is dead: the next round's evidence loads fly during this round's products
-        if (wbase + nthr < i_end) load_x(wbase + nthr, 0);
+        // (the next round's first chunk of evidence is already in flight)
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         if constexpr (!USE_LDS) {
@@ -1917,8 +1920,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             const long long nf4 = (n_factors + 3) & ~3;
             const long long side = (long long)kFastPtrs * sizeof(void*) +
                                    (long long)(kQueryThreads / kWave) * (kWave / Lp) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
-            long long budget = (long long)kLdsBudget - side - 1024;  // bytes
-            if (2 * side <= (long long)kLdsBudget) budget = std::min(budget, (long long)kLdsBudget / 2 - side - 1024);
+            const long long recb = (long long)n_factors * kRecFloats * 4;  // the records go to LDS too
+            long long budget = (long long)kLdsBudget - side - recb - 1024;  // bytes
+            if (2 * (side + recb) <= (long long)kLdsBudget)
+                budget = std::min(budget, (long long)kLdsBudget / 2 - side - recb - 1024);
             std::vector<std::pair<long long, int>> by_size;
             for (int f = 0; f < n_factors; ++f) {
                 long long rows = 1;
@@ -2159,6 +2164,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                             (size_t)(kQueryThreads / kWave) * (kWave / Lf) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
         const bool lds_ok = img_bytes + side <= (size_t)kLdsBudget;
         if (!lds_ok && P->use_lds) fast = false;  // keep one LDS mode per plan
+        // global tables: the LDS-copied small tables + the records + the side buffers must fit
+        if (!P->use_lds && (size_t)P->lds_tab_floats * 4 + (size_t)n_factors * kRecFloats * 4 + side > (size_t)kLdsBudget)
+            fast = false;
         if (fast) {
             P->fast = true;
             P->vpl = vpl;
@@ -2176,12 +2184,9 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                                        reinterpret_cast<const void*>(&k_query_staged<kModeRaw>)})
                     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget);
             }
-            P->fast_lds_bytes = ((P->use_lds ? img_bytes : (size_t)P->lds_tab_floats * 4) + side + 15) & ~size_t(15);
-            if (P->fast_lds_bytes > (size_t)kLdsBudget) {  // the LDS-table prefix was sized for this side buffer
-                const size_t b = P->fast_lds_bytes;
-                cbn_plan_destroy(P);
-                return set_err(CBN_E_HIP, "cbn_plan_create: internal error, fast-path LDS %zu B", b);
-            }
+            P->fast_lds_bytes =
+                ((P->use_lds ? img_bytes : (size_t)P->lds_tab_floats * 4 + (size_t)n_factors * kRecFloats * 4) + side +
+                 15) & ~size_t(15);
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
             P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
