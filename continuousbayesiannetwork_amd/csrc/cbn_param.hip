@@ -257,18 +257,21 @@ __device__ __forceinline__ float tanh_fast(float x) {
     const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);
     return copysignf(ax < 0.625f ? small : big, x);
 }
+// (the pair form works on the signed x: the odd polynomial's IEEE operations
+// are sign-symmetric, so it returns copysign(poly(|x|), x) bit for bit, and
+// |x| reaches the exponential as a source modifier -- no separate |x|)
 __device__ __forceinline__ f2 tanh_fast2(f2 x) {
-    const f2 ax = f2{fabsf(x.x), fabsf(x.y)};
-    const f2 z = ax * ax;
+    const f2 z = x * x;
     f2 p = fma2(z, f2s(-5.70498872745e-3f), f2s(2.06390887954e-2f));
     p = fma2(p, z, f2s(-5.37397155531e-2f));
     p = fma2(p, z, f2s(1.33314422036e-1f));
     p = fma2(p, z, f2s(-3.33332819422e-1f));
-    const f2 small = fma2(p * z, ax, ax);
-    const f2 t = ax * f2s(2.88539008177792681472f);
-    const f2 u = f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f2s(1.f);
+    const f2 small = fma2(p * z, x, x);
+    const f2 t = x * f2s(2.88539008177792681472f);
+    const f2 u = f2{__builtin_amdgcn_exp2f(fabsf(t.x)), __builtin_amdgcn_exp2f(fabsf(t.y))} + f2s(1.f);
     const f2 big = fma2(f2s(-2.f), f2{__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)}, f2s(1.f));
-    return f2{copysignf(ax.x < 0.625f ? small.x : big.x, x.x), copysignf(ax.y < 0.625f ? small.y : big.y, x.y)};
+    return f2{fabsf(x.x) < 0.625f ? small.x : copysignf(big.x, x.x),
+              fabsf(x.y) < 0.625f ? small.y : copysignf(big.y, x.y)};
 }
 
 // activation_map of neural_network.py:10-18 (torch CPU formulas)
