@@ -2509,6 +2509,16 @@ int cbn_plan_status(cbn_plan* plan, int32_t* status) {
     return CBN_OK;
 }
 
+int cbn_plan_check(cbn_plan* plan) {
+    if (!plan) return set_err(CBN_E_ARG, "cbn_plan_check: null plan");
+    if (plan->h_status && __atomic_load_n(plan->h_status, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(plan->h_status, 0u, __ATOMIC_RELEASE);
+        return set_err(CBN_E_TIMEOUT, "a single-launch call of this plan timed out in its grid barrier (another "
+                                      "stream held CUs its blocks needed): its rows are NaN");
+    }
+    return CBN_OK;
+}
+
 int64_t cbn_plan_fused_capacity(const cbn_plan* plan) { return plan ? fused_capacity(plan) : 0; }
 
 int32_t cbn_plan_flags(const cbn_plan* plan) {

@@ -289,6 +289,17 @@ class InferenceEngine:
         self._orders = {}
         self._fast = {}
 
+    def synchronize(self):
+        """Wait for this engine's calls on the current device and report a call
+        whose single-launch grid barrier timed out (its rows are NaN) NOW, as
+        NativeError(CBN_E_TIMEOUT) -- without this, the plan's next call reports
+        it.  Not in the reference (its infer has no grid barrier)."""
+        torch.cuda.synchronize()
+        lib = _native.load()
+        for p in self._plans.values():
+            if p.handle is not None and p.handle.value:
+                _native.check(lib.cbn_plan_check(p.handle), "cbn_plan_check")
+
     def __del__(self):
         try:
             for p in self._plans.values():

@@ -228,6 +228,14 @@ int cbn_plan_run_fold(cbn_plan* plan, int64_t n_queries, const float* const* evi
                       const uint32_t* fold_words, int32_t fold_n_words, int32_t flags, void* stream);
 int cbn_plan_status(cbn_plan* plan, int32_t* status);
 
+/* CBN_E_TIMEOUT (and clears the report) if a single-launch call of the plan
+ * timed out in its grid barrier since the last report, else CBN_OK: a read of
+ * the plan's host-mapped status word, no device round trip.  A caller that
+ * synchronised the stream of its calls learns of such a call at that point
+ * instead of on the plan's next cbn_plan_run.  Added in ABI 4 (round 3).
+ * No reference counterpart (the reference's infer has no grid barrier). */
+int cbn_plan_check(cbn_plan* plan);
+
 /* Which kernels serve the plan (bit set): diagnostics / bench labels. */
 #define CBN_PLAN_FAST 1        /* table fast path (k_query_fast / k_query_staged) */
 #define CBN_PLAN_LDS 2         /* the table image is staged in LDS (else read from L2 / HBM) */

@@ -89,6 +89,23 @@ def test_timeout_is_reported_on_next_call(gpu):
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
 
 
+def test_timeout_is_reported_at_synchronize(gpu):
+    """engine.synchronize() reports a timed-out fused call (simulated through
+    the test hook) at the caller's sync point, not on the plan's next call."""
+    data, cols, edges = chain_data(20, 32, 60000, 8, stay=0.8)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X19"]
+    ev = _t(sample_evidence(data, cols, names, 4096, 9), gpu)
+    a, _ = bn.infer("X19", ev, N_max=32)
+    bn.engine.synchronize()  # nothing to report
+    plan = next(iter(bn.engine._plans.values()))
+    _native.check(_native.load().cbn_debug_flag_timeout(plan.handle), "flag")
+    with pytest.raises(_native.NativeError, match="timed out"):
+        bn.engine.synchronize()
+    b, _ = bn.infer("X19", ev, N_max=32)  # reported once, then cleared
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
 def test_out_argument_is_validated(gpu):
     data, cols, edges = chain_data(6, 4, 3000, 5, stay=0.8)
     bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
