@@ -682,7 +682,7 @@ __device__ __forceinline__ void load_inputs(const InCol* __restrict__ cols, long
 
 // (table mode: a null column -- an input that is not evidence -- is not
 // loaded, a wave-uniform branch; its z is 0 until a free-parent combo sets it)
-struct alignas(16) PEv4 {
+struct PEv4 {  // (8-B aligned like the kernel-argument pointer table it views)
     const float* p[kTabIn];
 };
 __device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, unsigned qb, float (&z)[kMaxP]) {
