@@ -18,10 +18,19 @@ exchange the global max with one RCCL all-reduce of the block max words
 between the raw launch and the in-place scale, pipelined so a step's exchange
 overlaps the next step's launch (distributed.ShardedStepper;
 ``--serial-exchange`` for the unpipelined step, ``--sharded`` runs that N>1
-step at N=1 over a one-rank RCCL communicator).  ``value`` keeps every rank's
-normalised rows on that rank (the marginal tensor stays sharded); the step
-with the RCCL all-gather reassembly of the full tensor on every rank is timed
-after it and reported as ``value_gathered`` (``--gather`` swaps the two).
+step at N=1 over a one-rank RCCL communicator).  At N > 1 ``value`` is
+north_star's step: the shard's raw launch, the all-reduce + scale AND the RCCL
+all-gather that reassembles the full [Q, N] marginal tensor on every rank
+(``value_kind`` "gathered"); the step that leaves the tensor sharded is timed
+after it as ``value_rank_local`` (``--rank-local`` swaps the two).  The line
+carries DESIGN.md's ``projection`` for both at that N.  A rank that makes no
+host progress for ``--watchdog`` seconds prints its step / ring state / last
+collective and exits non-zero (distributed.Watchdog).
+
+``timing`` itemises ms_per_step: host enqueue time per step, the GPU-side
+event region, the same launches back-to-back with the queue held full (a
+kernel duration independent of the host), and what lies outside the region
+(first submit, final sync wake-up).
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` for the dominant
 kernel -- the single-launch fused query kernel at N=1 (the write pass when the
@@ -50,7 +59,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from continuousbayesiannetwork_amd import BayesianNetwork  # noqa: E402
-from continuousbayesiannetwork_amd.distributed import ShardedStepper  # noqa: E402
+from continuousbayesiannetwork_amd.distributed import ShardedStepper, Watchdog  # noqa: E402
 from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -73,7 +82,7 @@ def pmc_traffic(kernel: str):
     return None, None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -90,6 +99,17 @@ def parse():
     ap.add_argument("--two-pass", action="store_true", help="force the two-launch (max, write) path")
     ap.add_argument("--sharded", action="store_true",
                     help="run the N>1 step (raw launch + RCCL all-reduce + scale, pipelined) even at N=1")
+    ap.add_argument("--rank-local", action="store_true",
+                    help="N>1: time the step WITHOUT the all-gather reassembly as `value` (each rank keeps its "
+                         "normalised shard); by default `value` is north_star's step, with the RCCL all-gather of "
+                         "the [Q, N] marginal tensor on every rank, and the rank-local step is timed after it "
+                         "(value_rank_local)")
+    ap.add_argument("--fold", action="store_true",
+                    help="N>1 rank-local: fold each step's division into a later raw launch (cbn_plan_run_fold); "
+                         "default only on a one-rank communicator (--sharded at N=1)")
+    ap.add_argument("--watchdog", type=float, default=60.0,
+                    help="N>1: seconds without host progress (a step, a wait, a barrier) after which a rank prints "
+                         "its step index / ring state / last collective and exits non-zero")
     ap.add_argument("--serial-exchange", action="store_true",
                     help="N>1: no pipelining (each step's all-reduce + scale before the next raw launch)")
     ap.add_argument("--no-fold", action="store_true",
@@ -98,16 +118,13 @@ def parse():
     ap.add_argument("--exchange-every", type=int, default=8,
                     help="N>1: steps per all-reduce + scale group (1..8)")
     ap.add_argument("--gather", action="store_true",
-                    help="N>1: time the step WITH the all-gather reassembly of the [Q, N] marginal tensor on every "
-                         "rank as `value`; by default each rank keeps its normalised shard of the marginal tensor "
-                         "(the reassembly cannot scale: DESIGN.md, Multi-GPU) and the gathered step is measured "
-                         "after it and reported as value_gathered")
+                    help="--sharded at N=1: time the step with the (one-rank) all-gather reassembly as `value`")
     ap.add_argument("--skip-other", action="store_true",
                     help="N>1: do not time the other reassembly choice after the headline step (profiling runs)")
     ap.add_argument("--rebuild-tables", action="store_true",
                     help="re-run k_build_tables in every step (the factor tables are plan constants; by default "
                          "they are built once per plan, as in serving)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def free_port() -> int:
@@ -139,13 +156,15 @@ def check_world(gpus: int, env) -> int:
     return int(w)
 
 
-def launch_ranks(a, argv) -> int:
+def launch_ranks(a, argv, script: str = None) -> int:
     """``--gpus N > 1`` outside torch.distributed.run: start the N ranks as a
     CHILD process (never exec: nothing here has touched the GPU, and the
-    parent only waits) and return its exit code."""
+    parent only waits) and return its exit code (a rank that exits non-zero,
+    e.g. on its watchdog, makes torch.distributed.run stop the others and
+    return non-zero)."""
     import subprocess
 
-    cmd = rank_launch_command(a.gpus, argv, free_port())
+    cmd = rank_launch_command(a.gpus, argv, free_port(), script=script)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between the rank processes)
     print("bench.py: launching", " ".join(cmd), file=sys.stderr, flush=True)
@@ -207,6 +226,84 @@ def cpu_baseline(data, cols, edges, ev_np, target, N, budget_s):
                        f"{cores} worker processes (numpy, one chunk each) + the global-max division; {t:.2f} s")
 
 
+def step_modes(a, world: int) -> dict:
+    """What the timed region measures (``value``) and what is timed after it.
+
+    N > 1: north_star's configuration -- every rank runs its shard (one raw
+    launch + the RCCL all-reduce(MAX) of the block max words + scale) AND the
+    RCCL all-gather that reassembles the full [Q, N] marginal tensor on every
+    rank -- is ``value``; the rank-local step (each rank keeps its normalised
+    shard) is ``value_rank_local`` (``--rank-local`` swaps the two).  N = 1:
+    the fused single launch (``--sharded``: the N>1 step over a one-rank
+    communicator)."""
+    sharded = world > 1 or a.sharded
+    gather = (world > 1 and not a.rank_local) or (sharded and world == 1 and a.gather)
+    fold = a.fold or (world == 1 and not a.no_fold)  # fold ring: one-rank only unless asked (ADVICE r03)
+    kind = ("gathered" if gather else "rank_local") if sharded else "single_process"
+    other = ("rank_local" if gather else "gathered") if sharded and not a.skip_other else None
+    if sharded:
+        par = (f"query-shard x{world} + RCCL all-reduce(max) of the block max words"
+               + (", serial" if a.serial_exchange else ", overlapped with the next step's launch")
+               + (" + RCCL all-gather of the [Q, N] marginal tensor on every rank" if gather
+                  else " (marginal tensor left sharded: no all-gather)"))
+    else:
+        par = f"query-shard x{world}"
+    return dict(sharded=sharded, gather=gather, fold=fold, value_kind=kind, other_kind=other, parallelism=par)
+
+
+def projection(world: int) -> dict:
+    """DESIGN.md (Multi-GPU) bound on the gathered step: every rank receives
+    (N-1) x 8.4 MB of rows per step over its 7 xGMI links and writes N x 8.4 MB
+    of marginals -- a projection, not a measurement."""
+    rows_b = 65536 * 32 * 4
+    t_link = (world - 1) * rows_b / (XGMI_PEAK_GBS * 1e9)
+    t_write = world * rows_b / (HBM_PEAK_GBS * 1e9)
+    t_one = 10.3e-6
+    return {"gathered_x_vs_1gpu": round(world * t_one / max(t_one, t_link, t_write), 2),
+            "rank_local_x_vs_1gpu": round(world * t_one / 13.2e-6, 2) if world > 1 else 1.0,
+            "basis": "DESIGN.md Multi-GPU: gathered step >= max(10.3 us kernel, (N-1) x 8.4 MB over 7 x 153 GB/s, "
+                     "N x 8.4 MB written at 8 TB/s); rank-local ~13.2 us per step (12.2 measured at N=1 + ~1 us "
+                     "of collective interference)"}
+
+
+def reference_over_port():
+    """Ratio of the reference's own CPU path to the oracle port at equal cores
+    (profiles/r02_cpu_reference.json: 8 single-thread processes each), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02_cpu_reference.json")) as fh:
+            d = json.load(fh)
+        ref = max(r["queries_per_s"] for r in d["reference"] if r["threads"] * r["processes"] == 8)
+        port = max(r["queries_per_s"] for r in d["port"] if r["processes"] == 8)
+        return round(ref / port, 3)
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def backlogged_launch_us(step, K: int, stream) -> float:
+    """Average duration of K back-to-back steps with the launch queue full: the
+    stream is first held by a spin kernel long enough for the host to enqueue
+    all K steps, so the HIP events around them see no host gaps (a kernel
+    duration, comparable with rocprofv3's, whatever the host's enqueue speed)."""
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    torch.cuda._sleep(1_000_000)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    per_cycle_ms = ev[0].elapsed_time(ev[1]) / 1_000_000
+    t0 = time.perf_counter()
+    for _ in range(4):
+        step()
+    torch.cuda.synchronize()
+    host_ms = (time.perf_counter() - t0) / 4 * 1e3
+    torch.cuda._sleep(int(min(2e9, 3.0 * K * host_ms / max(per_cycle_ms, 1e-9) + 1e6)))
+    ev[2].record(stream)
+    for _ in range(K):
+        step()
+    ev[3].record(stream)
+    torch.cuda.synchronize()
+    return ev[2].elapsed_time(ev[3]) / K * 1e3
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -214,7 +311,8 @@ def main():
     world = check_world(a.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    sharded = world > 1 or a.sharded
+    modes = step_modes(a, world)
+    sharded, gather = modes["sharded"], modes["gather"]
     n, d, Q = a.nodes, a.card, a.queries
     target = f"X{n - 1}"
     data, cols, edges = chain_data(n, d, a.train_rows, 3, stay=0.8)
@@ -224,6 +322,7 @@ def main():
     if rank == 0 and not sharded and not a.no_cpu_baseline:
         # first, while no process has touched the GPU: its worker pool forks
         cpu = cpu_baseline(data, cols, edges, ev_np, target, d, a.cpu_seconds)
+    wd = None
     if sharded:
         torch.cuda.set_device(local)
         if "WORLD_SIZE" not in os.environ:  # --sharded outside torch.distributed.run: a one-rank group
@@ -231,6 +330,9 @@ def main():
                          ("WORLD_SIZE", "1")):
                 os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world > 1:
+            # bounded N>1 run: a rank stuck in a collective reports and exits
+            wd = Watchdog(a.watchdog, what="(bench.py N>1)")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -246,12 +348,13 @@ def main():
         batches.append({k: v[perm].contiguous().to(dev) for k, v in base.items()})
     it = [0]
     # N>1: one raw launch per step on the compute stream; the all-reduce(MAX)
-    # of the block max words + the in-place scale run on a comm stream, once per
-    # --exchange-every steps (8) for all of them, so the exchange overlaps the next steps' launches
-    # (distributed.ShardedStepper)
-    gather = sharded and a.gather
+    # of the block max words + the in-place scale (+ the all-gather) run on a
+    # comm stream, once per --exchange-every steps (8) for all of them, so the
+    # exchange overlaps the next steps' launches (distributed.ShardedStepper)
     stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                             force_exchange=sharded, gather=gather, fold=not a.no_fold)
+                             force_exchange=sharded, gather=gather, fold=modes["fold"], watchdog=wd)
+    if wd is not None:
+        wd.describe = lambda: stepper.describe()
 
     def step():
         ev = batches[it[0] % len(batches)]
@@ -263,10 +366,16 @@ def main():
             return rows
         return bn.infer(target, ev, N_max=d)
 
+    def barrier(what):
+        if wd is not None:
+            wd.beat(op=f"barrier ({what})")
+            stepper.last_op = f"dist.barrier ({what})"
+        dist.barrier()
+
     def timed_steps(K):
         """K steps between barriers + device syncs; max over ranks of the wall time."""
         if sharded:
-            dist.barrier()
+            barrier("before the second timed region")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(K):
@@ -274,23 +383,29 @@ def main():
         stepper.wait()
         torch.cuda.synchronize()
         if sharded:
-            dist.barrier()
+            barrier("after the second timed region")
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         return float(dt.item())
 
+    if wd is not None:
+        wd.arm(phase="warmup")
     random.seed(0)
     for _ in range(a.warmup):
         step()
+    stepper.wait()
     torch.cuda.synchronize()
 
     K = a.steps
     bn.engine.timing()  # drop warm-up timings
     fused = not sharded and not a.two_pass and bn.engine.fused_capacity(target, names, d) >= Q
+    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if wd is not None:
+        wd.beat(phase="timed region")
     if sharded:
-        dist.barrier()
+        barrier("before the timed region")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()  # the library launches on torch's current stream: these events bracket every launch
@@ -300,11 +415,13 @@ def main():
         # per-step event records cost it ~3 us per step)
         bn.engine.timed = not sharded and not fused and i % 8 == 7
         step()
+    t_enq = time.perf_counter()  # host done enqueueing the K steps
     stepper.wait()
     ev1.record()
     torch.cuda.synchronize()
+    t_sync = time.perf_counter()
     if sharded:
-        dist.barrier()
+        barrier("after the timed region")
     t1 = time.perf_counter()
     bn.engine.timed = False
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
@@ -313,13 +430,30 @@ def main():
     sec = float(dt.item())
     ms_per_step = sec / K * 1e3
     value = Q * world * K / sec
+    region_us = ev0.elapsed_time(ev1) * 1e3  # GPU-side: first event -> last event on the launch stream
+    timing = {"host_enqueue_us_per_step": round((t_enq - t0) / K * 1e6, 3),
+              "tail_us": round((t_sync - t_enq) * 1e6, 2),
+              "region_events_us_per_step": round(region_us / K, 3),
+              "outside_region_us": round((t_sync - t0) * 1e6 - region_us, 2)}
+    if sharded:
+        timing["barrier_us"] = round((t1 - t_sync) * 1e6, 2)
 
     roofline = None
     ntimed, tmax_ms, twrite_ms = bn.engine.timing() if not sharded else (0, 0.0, 0.0)
     bn.engine.check_status()
     if fused:
         # one launch per step: average launch duration = HIP-event time of the timed region / K
-        ntimed, twrite_ms = K, ev0.elapsed_time(ev1) / K
+        ntimed, twrite_ms = K, region_us / K * 1e-3
+        # the same launches with the queue kept full (no host gaps): a kernel duration
+        kb = backlogged_launch_us(step, max(K, 100), stream)
+        timing["backlogged_us_per_launch"] = round(kb, 3)
+        timing["gpu_idle_us_per_step"] = round(region_us / K - kb, 3)
+        timing["itemised"] = (f"{ms_per_step * 1e3:.2f} us/step = {kb:.2f} kernel (back-to-back) + "
+                              f"{region_us / K - kb:.2f} GPU idle inside the event region (launch gaps: host "
+                              f"enqueue {(t_enq - t0) / K * 1e6:.2f} us/step) + "
+                              f"{((t_sync - t0) * 1e6 - region_us) / K:.2f} outside it (first submit + final "
+                              f"sync wake-up, {(t_sync - t0) * 1e6 - region_us:.1f} us over {K} steps) + "
+                              f"{(t1 - t_sync) * 1e6 / K:.2f} after the sync")
     if ntimed:
         tmax, twrite = tmax_ms * 1e-3, twrite_ms * 1e-3
         n_cols = len(names)  # evidence columns read per query
@@ -345,35 +479,35 @@ def main():
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
         roofline["timing"] = ("HIP events on the launch stream around the whole timed region / K launches" if fused
                               else "HIP events around the launches of every 8th step (library-side)")
+        if fused:
+            kb = timing["backlogged_us_per_launch"] * 1e-6
+            roofline["avg_us_backlogged"] = round(kb * 1e6, 2)
+            roofline["frac_backlogged"] = round(bytes_q / kb / 1e9 / HBM_PEAK_GBS, 4)
         if not fused:
             roofline["first_launch_us"], roofline["second_launch_us"] = round(tmax * 1e6, 2), round(twrite * 1e6, 2)
-    step_info = None
     if sharded and gather and world > 1:
         # with the reassembly, each rank receives the other ranks' rows every
         # step over xGMI: (world - 1) x Q x 4N bytes -- the dominant transfer
-        t_step = ev0.elapsed_time(ev1) / K * 1e-3
+        t_step = region_us / K * 1e-6
         bytes_in = (world - 1) * Q * 4 * d
         achieved = bytes_in / t_step / 1e9
-        step_info = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
-                         frac=round(achieved / XGMI_PEAK_GBS, 4),
-                         what="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of the "
-                              "[Q, N] rows (per step)",
-                         avg_us=round(t_step * 1e6, 2), bytes_per_step=bytes_in,
-                         timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
-                                "rows received from the other ranks per step")
-        roofline = dict(step_info, kernel=step_info["what"], traffic=None, algorithmic_bytes_per_launch=bytes_in,
-                        timed_steps=K)
+        roofline = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / XGMI_PEAK_GBS, 4), traffic=None,
+                        kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of "
+                               "the [Q, N] rows (per step)",
+                        avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_in, timed_steps=K,
+                        timing="HIP events on rank 0's launch stream around the timed region / K steps; bytes = "
+                               "rows received from the other ranks per step")
     elif sharded:
-        # rank-local sharded step: ONE raw launch per step on the launch stream,
-        # which also divides an earlier step's rows by that step's all-reduced
-        # max (cbn_plan_run_fold; the group's all-reduce runs on the comm
-        # stream); algorithmic bytes of that launch = evidence in + raw rows out
-        # + the folded rows read and written back; duration = HIP events on
-        # the launch stream around the timed region / K (an upper bound on the
-        # launch: it includes the step's share of the launch gaps)
+        # rank-local sharded step: ONE raw launch per step on the launch stream
+        # (folded: it also divides an earlier step's rows by that step's
+        # all-reduced max, cbn_plan_run_fold; else k_scale_batch per group on
+        # the comm stream); algorithmic bytes of that launch = evidence in +
+        # raw rows out + the rows read and written back by the division;
+        # duration = HIP events on the launch stream around the timed region / K
         n_cols = len(names)
         bytes_step = Q * (4 * n_cols + 3 * 4 * d)
-        t_step = ev0.elapsed_time(ev1) / K * 1e-3
+        t_step = region_us / K * 1e-6
         achieved = bytes_step / t_step / 1e9
         folded = getattr(stepper, "_folded", False)
         kname = "k_query_staged<3>"
@@ -388,13 +522,15 @@ def main():
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
 
     other = None
-    if sharded and not a.skip_other:
-        # the same step with the other reassembly choice, for reference: the
-        # all-gather of the full [Q, N] tensor on every rank (value_gathered), or
-        # (with --gather) each rank keeping its rows (value_rank_local)
+    if modes["other_kind"] is not None:
+        # the same step with the other reassembly choice: each rank keeping its
+        # rows (value_rank_local) or, with --rank-local, the all-gather of the
+        # full [Q, N] tensor on every rank (value_gathered)
+        if wd is not None:
+            wd.beat(phase="second timed region (" + modes["other_kind"] + ")")
         stepper.close()
         stepper = ShardedStepper(bn, target, d, exchange_every=1 if a.serial_exchange else a.exchange_every,
-                                 force_exchange=True, gather=not gather, fold=not a.no_fold)
+                                 force_exchange=True, gather=not gather, fold=modes["fold"], watchdog=wd)
         for _ in range(a.warmup):
             step()
         stepper.wait()
@@ -415,6 +551,12 @@ def main():
         bn.engine.cache_tables = True
 
     if rank == 0:
+        if cpu is not None:
+            r = reference_over_port()
+            if r is not None:
+                cpu["reference_over_port"] = r
+                cpu["reference_over_port_source"] = ("profiles/r02_cpu_reference.json: the reference's own infer "
+                                                     "vs this port, 8 single-thread processes each, same queries")
         line = {
             "metric": "marginal queries/sec + achieved HBM GB/s, 20-node d=32 DAG, 65k-batch VE",
             "value": round(value, 1), "unit": "queries/s", "n_gpus": world, "steps": K, "warmup": a.warmup,
@@ -422,26 +564,28 @@ def main():
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded chain samples; BruteForce fit)",
             "config": {"workload": f"chain{n}_d{d}: BayesianNetwork.infer target {target}, evidence on the other "
                                    f"{n - 1} nodes, N_max={d}", "queries_per_gpu": Q, "global_batch": Q * world,
-                       "parallelism": f"query-shard x{world}" + (
-                           " + RCCL all-reduce(max) of the block max words" + (
-                               ", serial" if a.serial_exchange else ", overlapped with the next step's launch") + (
-                               " + RCCL all-gather of the [Q, N] marginal tensor on every rank" if gather else "")
-                           if sharded else "")},
-            "roofline": roofline, "cpu_baseline": cpu,
+                       "parallelism": modes["parallelism"]},
+            "value_kind": modes["value_kind"],
+            "roofline": roofline, "cpu_baseline": cpu, "timing": timing,
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
             "evidence_batches": len(batches),
         }
+        if world > 1:
+            line["projection"] = projection(world)
         if cold is not None:
             line["value_rebuild_tables"] = round(cold, 1)
         if other is not None:
-            # same step, each rank keeps its own rows / every rank all-gathers the full tensor
-            line["value_gathered" if not gather else "value_rank_local"] = round(other, 1)
+            line["value_" + modes["other_kind"]] = round(other, 1)
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+            if cpu.get("reference_over_port"):
+                line["speedup_vs_reference_cpu"] = round(value / (cpu["value"] * cpu["reference_over_port"]), 1)
         assert line["n_gpus"] == a.gpus, (line["n_gpus"], a.gpus)
         print(json.dumps(line), flush=True)
     if sharded:
         stepper.close()
+        if wd is not None:
+            wd.close()
         dist.destroy_process_group()
 
 

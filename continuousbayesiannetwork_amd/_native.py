@@ -13,6 +13,8 @@ import os
 
 import torch  # noqa: F401  (must be imported before the HIP library)
 
+from . import _buildstamp
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
 
@@ -175,6 +177,16 @@ class NativeError(RuntimeError):
     pass
 
 
+def _check_stamp(path: str, digest: str) -> None:
+    """Refuse a library not built from this tree's sources (its content stamp,
+    written by __graft_entry__.build(), differs or is missing)."""
+    got = _buildstamp.read_stamp(path)
+    if got != digest:
+        raise NativeError(
+            f"{path} was not built from this tree's sources (stamp {got or 'missing'} != {digest[:16]}...): "
+            "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
+
+
 def load() -> ctypes.CDLL:
     """Load (once) and return the HIP library; raise if it is not built."""
     global _lib
@@ -183,6 +195,8 @@ def load() -> ctypes.CDLL:
             raise NativeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(no CPU fallback exists for the HIP inference path)")
+        if not os.environ.get("CBN_LIB_PATH"):  # (diagnostic variant builds carry no stamp)
+            _check_stamp(LIB_PATH, _buildstamp.lib_digest())
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
             fn = getattr(lib, name)
@@ -208,6 +222,7 @@ def load_host():
         import importlib.machinery
         import importlib.util
 
+        _check_stamp(HOST_PATH, _buildstamp.host_digest())
         loader = importlib.machinery.ExtensionFileLoader("_cbn_host", HOST_PATH)
         spec = importlib.util.spec_from_file_location("_cbn_host", HOST_PATH, loader=loader)
         mod = importlib.util.module_from_spec(spec)

@@ -481,6 +481,7 @@ class Stepper {
     void wait() { check_(ring_.wait()); }
     void synchronize() {
         check_(ring_.flush());
+        py::gil_scoped_release nogil;  // a watchdog thread may need to report a stuck peer
         CBN_HIP_OK(hipStreamSynchronize(ring_.ops().cs.stream()));
     }
     uintptr_t comm_stream() { return reinterpret_cast<uintptr_t>(ring_.ops().cs.stream()); }
@@ -824,6 +825,7 @@ struct FoldHipOps {
     void record(int set) { CBN_HIP_OK(hipEventRecord(ready_ev[set], A())); }
     bool passed(int set, bool block) {
         if (block) {
+            py::gil_scoped_release nogil;  // (watchdog: see Stepper::synchronize)
             CBN_HIP_OK(hipEventSynchronize(ready_ev[set]));
             return true;
         }
@@ -915,6 +917,7 @@ class FoldStepper {
     void wait() { check_(ring_.wait()); }
     void synchronize() {
         check_(ring_.wait());
+        py::gil_scoped_release nogil;
         CBN_HIP_OK(hipStreamSynchronize(ring_.ops().A()));
     }
     int64_t steps() const { return ring_.steps(); }

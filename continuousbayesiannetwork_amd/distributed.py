@@ -10,7 +10,11 @@ rank keeps the rows it owns.
 """
 from __future__ import annotations
 
+import os
 import random
+import sys
+import threading
+import time
 from contextlib import contextmanager
 from typing import Callable, Dict, Optional, Tuple
 
@@ -20,6 +24,74 @@ import torch.distributed as dist
 from .base.parameter_learning import GENERATION
 
 _RAW = 8  # CBN_RUN_RAW (include/cbn_amd.h)
+
+
+class Watchdog:
+    """Bound on a multi-rank run: a rank whose host makes no progress for
+    ``bound_s`` seconds (a peer that stopped issuing steps leaves it blocked
+    in a collective or a device wait) prints what it was doing and exits the
+    process with ``code`` (``os._exit``: no re-exec, no retry, no cleanup that
+    could block on the dead collective).  The launcher then sees a non-zero
+    rank and returns non-zero.
+
+    ``beat(**state)`` records progress (and what the rank is doing);
+    ``describe`` (optional) adds live state -- a ShardedStepper's ring -- to
+    the report.  The every-rank exchange this guards is the reference's one
+    global max (bayesian_network.py:296): every rank must pair it each step.
+    Blocking native waits release the GIL (csrc/host_fast.cpp), so the thread
+    runs while the main thread is stuck in one."""
+
+    def __init__(self, bound_s: float, what: str = "", describe: Optional[Callable[[], str]] = None,
+                 code: int = 3, stream=None):
+        self.bound = float(bound_s)
+        self.what = what
+        self.describe = describe
+        self.code = code
+        self.stream = stream if stream is not None else sys.stderr
+        self.state: Dict[str, object] = {}
+        self._last = time.monotonic()
+        self._armed = False
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="cbn-watchdog", daemon=True)
+        self._thread.start()
+
+    def arm(self, **state):
+        self.beat(**state)
+        self._armed = True
+
+    def disarm(self):
+        self._armed = False
+
+    def beat(self, **state):
+        self.state.update(state)
+        self._last = time.monotonic()
+
+    def close(self):
+        self._armed = False
+        self._stop.set()
+        self._thread.join(timeout=5)
+
+    def report(self) -> str:
+        rank = os.environ.get("RANK", "?")
+        world = os.environ.get("WORLD_SIZE", "?")
+        parts = [f"[cbn watchdog] rank {rank}/{world}: no progress for {time.monotonic() - self._last:.1f} s "
+                 f"(bound {self.bound:.1f} s) {self.what}".rstrip(),
+                 "  state: " + ", ".join(f"{k}={v}" for k, v in self.state.items())]
+        if self.describe is not None:
+            try:
+                parts.append("  " + self.describe())
+            except Exception as e:  # the report must not fail on a half-torn-down stepper
+                parts.append(f"  (describe failed: {e!r})")
+        return "\n".join(parts)
+
+    def _run(self):
+        tick = min(1.0, max(0.05, self.bound / 8))
+        while not self._stop.wait(tick):
+            if self._armed and time.monotonic() - self._last > self.bound:
+                try:
+                    print(self.report(), file=self.stream, flush=True)
+                finally:
+                    os._exit(self.code)
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -234,12 +306,21 @@ class ShardedStepper:
     """
 
     def __init__(self, bn, target_node: str, N_max: int = 16, group=None, exchange_every: int = 4,
-                 force_exchange: bool = False, gather: bool = False, fold: bool = True):
+                 force_exchange: bool = False, gather: bool = False, fold: Optional[bool] = None,
+                 watchdog: Optional[Watchdog] = None):
         self.bn, self.target, self.N_max, self.group = bn, target_node, N_max, group
+        multi = dist.is_initialized() and dist.get_world_size(group) > 1
         # rank-local steps on staged plans: each step's division by its global
         # max runs inside a later raw launch (cbn_plan_run_fold, FoldStepper)
-        # instead of a separate scale launch
-        self.fold = fold
+        # instead of a separate scale launch.  Default: only on a one-rank
+        # communicator -- the fold ring's host hand-off has not yet run against
+        # real peers on GPUs (tests/test_gpu_multi.py pins it when >= 2 GPUs
+        # are visible), so with peers the separate batched scale is used
+        self.fold = (not multi) if fold is None else fold
+        # progress reporting for a bounded multi-rank run (bench.py)
+        self.watchdog = watchdog
+        self.n_steps = 0
+        self.last_op = "none"
         # steps per exchange group: <= 8 for the separate batched scale (one
         # cbn_scale_batch per group), <= 32 when the scales are folded
         self.G_req = max(1, exchange_every)
@@ -315,6 +396,9 @@ class ShardedStepper:
         ``shard_bounds``; None = equal shards), otherwise this rank's rows."""
         eng = self.bn.engine
         c = self._c
+        self.n_steps += 1
+        if self.watchdog is not None:
+            self.watchdog.beat(step=self.n_steps)
         if c is not None and GENERATION[0] == eng._gen and eng.epoch == self._epoch and self._folded:
             # hot path (rank-local, folded): one native call
             fp = self._fp
@@ -374,13 +458,29 @@ class ShardedStepper:
         tdom = fp.tdom.get(res.shape[0])
         return res, (tdom if tdom is not None else self._tdom(fp, res.shape[0]))
 
+    def describe(self) -> str:
+        """One line of ring state for a watchdog report."""
+        c = self._c
+        kind = "none" if c is None else ("fold ring" if self._folded else "step ring")
+        ring = ""
+        if c is not None:
+            ring = f", native steps={c.steps()}, group={c.group()}"
+            if self._folded:
+                ring += f", unfinished={c.unfinished()}"
+        return (f"stepper: {kind}, world={self.world}, rank={self.rank}, G={self.G}, gather={self.gather}, "
+                f"serial={self._serial}, steps={self.n_steps}{ring}, last collective/wait={self.last_op}")
+
     def wait(self):
         """Make the current stream wait for every enqueued exchange + scale (+ gathers)."""
         if self._c is not None:
+            self.last_op = f"wait() after step {self.n_steps} (flushes the partial group's all-reduce)"
             self._c.wait()
+            if self.watchdog is not None:
+                self.watchdog.beat(op="wait done")
 
     def synchronize(self):
         if self._c is not None:
+            self.last_op = f"synchronize() after step {self.n_steps}"
             self._c.synchronize()
 
     def close(self):

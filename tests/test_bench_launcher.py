@@ -48,3 +48,100 @@ def test_mismatched_launch_exits_nonzero():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
+
+
+def test_n_gt_1_value_is_the_gathered_step():
+    """At N > 1 ``value`` is north_star's step (shard + all-reduce + the RCCL
+    all-gather of the marginal tensor) and the rank-local step is reported
+    beside it; --rank-local swaps them; N = 1 is the fused single launch."""
+    m = bench.step_modes(bench.parse(["--gpus", "2"]), 2)
+    assert m["sharded"] and m["gather"] and m["value_kind"] == "gathered"
+    assert "all-gather" in m["parallelism"] and m["other_kind"] == "rank_local"
+    assert not m["fold"]  # fold ring with real peers: off until pinned on >= 2 GPUs (ADVICE r03)
+    m = bench.step_modes(bench.parse(["--gpus", "2", "--rank-local"]), 2)
+    assert not m["gather"] and m["value_kind"] == "rank_local" and m["other_kind"] == "gathered"
+    assert "no all-gather" in m["parallelism"]
+    m = bench.step_modes(bench.parse([]), 1)
+    assert not m["sharded"] and m["value_kind"] == "single_process" and m["other_kind"] is None
+    m = bench.step_modes(bench.parse(["--sharded"]), 1)
+    assert m["sharded"] and not m["gather"] and m["fold"]
+    p = bench.projection(8)
+    assert p["gathered_x_vs_1gpu"] < 2.0 < p["rank_local_x_vs_1gpu"]
+
+
+STANDIN_MODES = """
+import json, os, sys
+sys.path.insert(0, {root!r})
+import bench
+world = bench.check_world(2, os.environ)
+m = bench.step_modes(bench.parse(["--gpus", "2"]), world)
+line = {{"n_gpus": world, "value_kind": m["value_kind"], "config": {{"parallelism": m["parallelism"]}}}}
+line["value_" + m["other_kind"]] = 1.0
+open(os.path.join(sys.argv[1], "line" + os.environ["RANK"]), "w").write(json.dumps(line))
+"""
+
+
+def test_two_rank_launch_line_names_the_all_gather(tmp_path):
+    """Through the 2-rank launch bench.py uses: each rank's line names the
+    all-gather in ``parallelism`` and carries ``value_rank_local``."""
+    import json
+
+    script = tmp_path / "modes.py"
+    script.write_text(STANDIN_MODES.format(root=ROOT))
+    cmd = bench.rank_launch_command(2, [str(tmp_path)], bench.free_port(), script=str(script))
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    for r in (0, 1):
+        line = json.loads((tmp_path / f"line{r}").read_text())
+        assert line["n_gpus"] == 2 and line["value_kind"] == "gathered"
+        assert "all-gather" in line["config"]["parallelism"] and "value_rank_local" in line
+
+
+STANDIN_STALL = """
+import os, sys, time
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+from continuousbayesiannetwork_amd.distributed import Watchdog
+dist.init_process_group("gloo")
+rank = dist.get_rank()
+wd = Watchdog({bound}, what="(stand-in N>1 bench)")
+wd.arm(phase="timed region")
+x = torch.zeros(1)
+for i in range(1, 1000):
+    if rank == 1 and i > 3:
+        time.sleep(600)  # rank 1 stops issuing steps
+    wd.beat(step=i, op="all_reduce(max) of the block max words")
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+print("unreachable", flush=True)
+"""
+
+
+def test_watchdog_ends_a_stalled_two_rank_run(tmp_path):
+    """Rank 1 stops issuing steps: rank 0, blocked in the step's collective,
+    reports its step index / last collective within the bound and exits
+    non-zero; torch.distributed.run stops rank 1 and bench.launch_ranks
+    returns the failure."""
+    import time
+
+    script = tmp_path / "stall.py"
+    script.write_text(STANDIN_STALL.format(root=ROOT, bound=3.0))
+    a = bench.parse(["--gpus", "2"])
+    log = tmp_path / "err.txt"
+    t0 = time.monotonic()
+    with open(log, "w") as fh:
+        import contextlib
+
+        with contextlib.redirect_stderr(fh):
+            # launch_ranks inherits this process's fds: capture at the fd level
+            rc = subprocess.run([sys.executable, "-c",
+                                 "import sys; sys.path.insert(0, %r); import bench; "
+                                 "sys.exit(bench.launch_ranks(bench.parse(['--gpus', '2']), [], script=%r))"
+                                 % (ROOT, str(script))],
+                                stdout=fh, stderr=subprocess.STDOUT, timeout=180).returncode
+    dt = time.monotonic() - t0
+    err = log.read_text()
+    assert a.gpus == 2
+    assert rc != 0, err
+    assert "[cbn watchdog] rank 0/2" in err and "step=4" in err and "all_reduce" in err, err
+    assert "unreachable" not in err
+    assert dt < 120, dt
