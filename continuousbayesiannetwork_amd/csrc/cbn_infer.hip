@@ -1019,6 +1019,234 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 }
 
 // ---------------------------------------------------------------------------
+// Column-staged fast kernel (round 4; non-paired table plans: configs[2],
+// configs[4]).  k_query_fast indexes evidence per (factor, observed parent):
+// every lane issues kFastObs loads per factor (absent parents included, so the
+// waits stay counted) and maps each to a domain index, in chunks of kLoc
+// factors -- for ALARM-like X35 (26 factors, 36 evidence columns, one lane
+// per query) that is 104 loads and 104 index computations per query in four
+// dependent rounds, ~15.7 us of a 31 us launch.  But a domain index depends
+// only on the EVIDENCE SLOT, not on the factor: here the L lanes of a query
+// split its ns slots, load each column once (all loads of a chunk in flight),
+// map the value to its domain index (dense: the value; else a binary search
+// in the slot's sorted domain) and store it as an int16 in LDS
+// ([slot][query of the block], -1 off-domain).  The product loop then forms
+// each factor's row offset from its parents' indices (LDS reads, the record
+// broadcast from LDS) right before gathering the row: no offset buffer, no
+// per-factor evidence reloads.  Same factor order, same products, same
+// outputs as k_query_fast (bit-identical); modes as there.
+constexpr int kColChunk = 40;  // slot loads in flight per lane (ns <= 40 per lane: one round trip)
+constexpr int kColKB = 6;      // factors' rows in flight per gather batch
+
+template <int VPL, bool USE_LDS, int MODE>
+__global__ void __launch_bounds__(kQueryThreads)
+k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats,
+             FPtrsT<kFastPtrsSmall> sp, long long Q, long long per, int N, int RS, int L,
+             unsigned* __restrict__ sync, unsigned epoch, const unsigned* __restrict__ max_in, int n_max,
+             unsigned* __restrict__ max_out, float* __restrict__ out, int lds_tab, unsigned long long lmask0,
+             unsigned long long lmask1) {
+    CBN_STAMP_INIT;
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float* simg = reinterpret_cast<float*>(smem4);
+    if (USE_LDS) lds_tab = 0;
+    // LDS: [tables (USE_LDS: the whole image) | small tables][records][slot records][slot ptrs][idx][wave max]
+    const int recs_floats = nf * kRecFloats + ns * 4;  // FastRec[nf] then QSlot[ns], contiguous in the image
+    const int lrec = USE_LDS ? rec_off : lds_tab;      // float offset of the records in LDS
+    const float** sptr = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : lds_tab + recs_floats));
+    const int tid = threadIdx.x;
+    const int nthr = kQueryThreads;
+    const int QB = nthr / L;  // queries per block round
+    short* sidx = reinterpret_cast<short*>(sptr + ((ns + 1) & ~1));  // [ns][QB]
+    float* wmax = reinterpret_cast<float*>(sidx + (((size_t)ns * QB + 1) & ~size_t(1)));
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    const long long q0 = (long long)blockIdx.x * per;
+    const long long q1 = q0 + per < Q ? q0 + per : Q;
+    if (USE_LDS) lds_dma_copy(gimage, smem4, image_floats / 4);
+    else {
+        if (lds_tab > 0) lds_dma_copy(gimage, smem4, lds_tab / 4);
+        lds_dma_copy(gimage + rec_off, smem4 + lds_tab / 4, recs_floats / 4);
+    }
+    if (tid < ns) sptr[tid] = sp.p[tid];
+    CBN_STAMP(1);
+    __syncthreads();
+    CBN_STAMP(2);
+    const float* img = USE_LDS ? simg : gimage;
+    const FastRec* rec = reinterpret_cast<const FastRec*>(simg + lrec);
+    const QSlot* srec = reinterpret_cast<const QSlot*>(simg + lrec + nf * kRecFloats);
+
+    float maxv = 1.f;
+    if (MODE == kModeWrite) {
+        unsigned m = 0;
+        for (int i = lane; i < n_max; i += kWave) m = max(m, max_in[i]);
+        m = wave_max_u(m);
+        maxv = __uint_as_float(m);
+        if (max_out && blockIdx.x == 0 && tid == 0) *max_out = m;
+    }
+    float lmax = 0.f;
+    const int ql = tid / L;        // this lane's query within the block round
+    const int l = tid - ql * L;    // lane within the query
+    const int nsl = (ns - l + L - 1) / L;  // slots this lane indexes: l, l + L, ...
+    int col[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) col[v] = (l * VPL + v) * 4;
+    constexpr int NV = 4 * VPL;
+    float acc[NV];
+    long long fq = -1;
+    bool first = true;
+    for (long long qb = q0; qb < q1; qb += QB) {  // block-uniform rounds
+        const long long qq = qb + ql;
+        const bool valid = qq < q1;
+        const long long q = valid ? qq : q0;
+        if (first) CBN_STAMP(3);
+        // index phase: this lane's slots, kColChunk loads in flight per chunk
+        for (int c0 = 0; c0 < nsl; c0 += kColChunk) {  // (uniform across the wave unless ns % L)
+            float x[kColChunk];
+#pragma unroll
+            for (int k = 0; k < kColChunk; ++k) {
+                int s = l + (c0 + k) * L;
+                s = s < ns ? s : ns - 1;  // unconditional loads: the compiler's waits stay counted
+                x[k] = gload(sptr[s], q);
+            }
+#pragma unroll
+            for (int k = 0; k < kColChunk; ++k) {
+                const int s = l + (c0 + k) * L;
+                if (c0 + k < nsl) {
+                    const QSlot sr = srec[s];
+                    const float xv = x[k];
+                    int i;
+                    if (sr.dense) {
+                        i = (int)xv;
+                        i = (xv >= 0.f && xv < (float)sr.card && (float)i == xv) ? i : -1;
+                    } else {
+                        i = bsearch_eq(img + sr.dom_off, sr.card, xv);
+                    }
+                    sidx[s * QB + ql] = (short)i;
+                }
+            }
+        }
+        // the L lanes of a query are in one wave: a wave-local LDS fence
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        if (first) CBN_STAMP(4);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        for (int f0 = 0; f0 < nf; f0 += kColKB) {
+            int oo[kColKB];
+#pragma unroll
+            for (int k = 0; k < kColKB; ++k) {
+                const int f = f0 + k;
+                int o = -1;
+                if (f < nf) {
+                    const FastRec& r = rec[f];
+                    o = r.table_off;
+                    int row = 0;
+                    bool ok = true;
+#pragma unroll
+                    for (int p = 0; p < kFastObs; ++p) {
+                        if (p < r.n_obs) {
+                            const int i = sidx[r.slot[p] * QB + ql];
+                            ok &= i >= 0;
+                            row = row * (r.card[p] & (kDenseBit - 1)) + (i < 0 ? 0 : i);
+                        }
+                    }
+                    o = ok ? o + row * RS : -1;
+                }
+                oo[k] = o;
+            }
+            float4 t[kColKB][VPL];
+#pragma unroll
+            for (int k = 0; k < kColKB; ++k) {
+                const int o = oo[k];
+                const int fk = f0 + k;
+                const bool in_lds = USE_LDS || (fk < nf && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0));
+                const float* base = in_lds ? simg : img;
+                const float4* row = reinterpret_cast<const float4*>(base + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < kColKB; ++k) {
+                if (f0 + k < nf) {
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        acc[4 * v + 0] = acc[4 * v + 0] * t[k][v].x;
+                        acc[4 * v + 1] = acc[4 * v + 1] * t[k][v].y;
+                        acc[4 * v + 2] = acc[4 * v + 2] * t[k][v].z;
+                        acc[4 * v + 3] = acc[4 * v + 3] * t[k][v].w;
+                    }
+                }
+            }
+        }
+        if (first) CBN_STAMP(5);
+        if (valid) {
+            if (MODE == kModeFused) fq = q;
+            if (MODE == kModeWrite) {
+                float* o = out + q * N;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                        acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
+            } else if (MODE == kModeRaw) {
+                float* o = out + q * N;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    *reinterpret_cast<float4*>(o + col[v]) =
+                        make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
+            }
+        }
+        // the next round rewrites this query slot's indices (lanes of one wave)
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (first) CBN_STAMP(6);
+        first = false;
+    }
+    CBN_STAMP(7);
+    if (MODE == kModeMax || MODE == kModeRaw) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
+            max_out[blockIdx.x] = __float_as_uint(m);
+        }
+        if (blockIdx.x == 0)
+            for (int i = (int)gridDim.x + tid; i < n_max; i += nthr) max_out[i] = 0u;
+    }
+    if (MODE == kModeFused) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (wid == 0) {
+            const int nw = nthr / kWave;
+            const unsigned gm = slot_barrier_max(sync, epoch, wave_max(lane < nw ? wmax[lane] : 0.f));
+            if (lane == 0) {
+                wmax[0] = __uint_as_float(gm);
+                if (blockIdx.x == 0 && max_out) *max_out = gm;
+            }
+        }
+        CBN_STAMP(8);
+        __syncthreads();
+        CBN_STAMP(9);
+        maxv = wmax[0];
+        if (fq >= 0) {
+            float* o = out + fq * N;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v)
+                *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                    acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
+        }
+        CBN_STAMP(10);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Staged fast kernel: the paired N = 32 layout in LDS (four lanes per query,
 // eight columns per lane, <= 32 factors), all four modes.  A block walks its
 // query range in rounds of kSR = 256 queries (16 waves x 16 queries).
@@ -1592,6 +1820,13 @@ FPtrsT<NP> fast_ptrs(const cbn_plan* p, const EvPtrs& ev, int first_factor = 0) 
     return fp;
 }
 
+// this call's column pointer of every evidence slot (k_query_cols)
+FPtrsT<kFastPtrsSmall> slot_ptrs(const cbn_plan* p, const EvPtrs& ev) {
+    FPtrsT<kFastPtrsSmall> sp;
+    for (int i = 0; i < kFastPtrsSmall; ++i) sp.p[i] = i < p->ns ? ev.p[i] : nullptr;
+    return sp;
+}
+
 // one fast-kernel launch with the pointer table sized to the plan
 template <int VPL, bool LDS, int MODE, int NP>
 void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
@@ -1620,6 +1855,13 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
                            fj, fast_ptrs<kFastPtrsSmall>(p, ev, p->prefix));
         return;
     }
+    if (p->cols) {
+        hipLaunchKernelGGL((k_query_cols<VPL, LDS, MODE>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
+                           p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, slot_ptrs(p, ev), Q,
+                           (Q + blocks - 1) / blocks, p->N, p->RS, L, p->d_sync, epoch, max_in, n_max, max_out, out,
+                           p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
+        return;
+    }
     if (p->nf * kFastObs <= kFastPtrsSmall)
         launch_fast_np<VPL, LDS, MODE, kFastPtrsSmall>(p, blocks, s, ev, Q, L, epoch, max_in, n_max, max_out, out);
     else
@@ -1627,7 +1869,8 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
 }
 
 template <int VPL, bool LDS, int MODE>
-const void* fast_kernel_fn(int nf) {
+const void* fast_kernel_fn(int nf, bool cols = false) {
+    if (cols) return reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE>);
     return nf * kFastObs <= kFastPtrsSmall ? reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>)
                                            : reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>);
 }
@@ -1637,6 +1880,8 @@ void allow_fast_lds(int bytes) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
@@ -2041,6 +2286,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     }
     const long long rec_off = off;  // FastRec array (fast path), copied to LDS with the tables
     off += (long long)n_factors * kRecFloats;
+    off += (long long)ns * 4;  // QSlot array right after it (k_query_cols: one LDS-DMA for both)
     if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
 
     cbn_plan* P = new cbn_plan();
@@ -2187,10 +2433,31 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             P->fast_lds_bytes =
                 ((P->use_lds ? img_bytes : (size_t)P->lds_tab_floats * 4 + (size_t)n_factors * kRecFloats * 4) + side +
                  15) & ~size_t(15);
+            // column-staged kernel (k_query_cols): non-paired plans whose slot
+            // indices fit int16 and whose per-slot index buffer fits LDS
+            if (!P->staged && !P->paired && ns <= kFastPtrsSmall && !getenv("CBN_NO_COLS")) {
+                bool ok_c = true;
+                for (int sl = 0; sl < ns; ++sl) ok_c = ok_c && slot_card[sl] <= 32767;
+                for (int f = 0; f < n_factors && ok_c; ++f)
+                    for (int q = 0; q < recs[f].n_obs; ++q)
+                        ok_c = ok_c && (recs[f].card[q] & (kDenseBit - 1)) == slot_card[recs[f].slot[q]];
+                const size_t QBc = (size_t)kQueryThreads / Lf;
+                const size_t cols_bytes =
+                    ((P->use_lds ? img_bytes
+                                 : (size_t)P->lds_tab_floats * 4 + ((size_t)n_factors * kRecFloats + (size_t)ns * 4) * 4) +
+                     (size_t)((ns + 1) & ~1) * sizeof(void*) + (((size_t)ns * QBc + 1) & ~size_t(1)) * 2 +
+                     (kQueryThreads / kWave) * 4 + 64 + 15) & ~size_t(15);
+                if (ok_c && cols_bytes <= (size_t)kLdsBudget) {
+                    P->cols = true;
+                    P->fast_lds_bytes = cols_bytes;
+                }
+            }
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
             P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
-                hipSuccess) {
+                    hipSuccess ||
+                (ns > 0 && hipMemcpy(P->d_image + rec_off + (long long)n_factors * kRecFloats, qs.data(),
+                                     sizeof(QSlot) * ns, hipMemcpyHostToDevice) != hipSuccess)) {
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
             }
@@ -2203,10 +2470,10 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 allow_fast_lds<2, false, kModeFused>(kLdsBudget);
                 int nb = 0;
                 const void* fn = P->staged ? reinterpret_cast<const void*>(&k_query_staged<kModeFused>)
-                                 : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors)
-                                                          : fast_kernel_fn<1, true, kModeFused>(n_factors))
-                                              : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors)
-                                                          : fast_kernel_fn<1, false, kModeFused>(n_factors));
+                                 : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors, P->cols)
+                                                          : fast_kernel_fn<1, true, kModeFused>(n_factors, P->cols))
+                                              : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors, P->cols)
+                                                          : fast_kernel_fn<1, false, kModeFused>(n_factors, P->cols));
                 const size_t lb = P->staged ? P->staged_lds_bytes : P->fast_lds_bytes;
                 if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, lb) == hipSuccess && nb >= 1)
                     P->fused_ok = true;
@@ -2526,7 +2793,8 @@ int32_t cbn_plan_flags(const cbn_plan* plan) {
     return (plan->fast ? CBN_PLAN_FAST : 0) | (plan->use_lds ? CBN_PLAN_LDS : 0) |
            (plan->paired ? CBN_PLAN_PAIRED : 0) | (plan->staged ? CBN_PLAN_STAGED : 0) |
            (plan->fused_ok ? CBN_PLAN_FUSED : 0) | (plan->param ? CBN_PLAN_PARAMETRIC : 0) |
-           (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0) | (plan->direct ? CBN_PLAN_DIRECT : 0);
+           (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0) | (plan->direct ? CBN_PLAN_DIRECT : 0) |
+           (plan->cols ? CBN_PLAN_COLS : 0);
 }
 
 int32_t cbn_plan_max_words(const cbn_plan* plan) {

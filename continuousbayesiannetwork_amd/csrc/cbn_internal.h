@@ -84,6 +84,7 @@ struct cbn_plan {
     bool paired = false;         // N = 32 bank-half layout (RS = 64, factor f in half f & 1), VPL 2 in LDS
     bool staged = false;         // paired plans of <= 32 factors: k_query_staged (evidence staged by factor)
     size_t staged_lds_bytes = 0;
+    bool cols = false;           // non-paired fast plans: k_query_cols (evidence indexed per slot, round 4)
     int zero_off = -1;
     int prefix = 0;              // staged plans: leading 1-row factors folded into factor `prefix` (k_merge_prefix)
     int prefix_offs[9] = {};     // table offsets of factors 0..prefix

@@ -245,6 +245,7 @@ int cbn_plan_check(cbn_plan* plan);
 #define CBN_PLAN_PARAMETRIC 32 /* parametric CPDs (cbn_param.hip) */
 #define CBN_PLAN_VPL2 64       /* 8 output columns per lane */
 #define CBN_PLAN_DIRECT 128    /* direct plan (cbn_plan_create_direct) */
+#define CBN_PLAN_COLS 256      /* k_query_cols (evidence indexed once per slot; non-paired table plans) */
 int32_t cbn_plan_flags(const cbn_plan* plan);
 
 /* Test hook: mark the plan as if a single-launch call had timed out in its

@@ -172,6 +172,38 @@ def grid_data(S, seed, side=10, d=64, keep=0.8, noise=2):
     return X.astype(np.float32), [f"X{i}" for i in range(n)], edges
 
 
+def grid_rows_data(S, seed, side=10, d=64, keep_even=0.9, keep_odd=1.0):
+    """configs[4]'s grid DAG (same edges as ``grid_data``) with data shaped for
+    evidence on the EVEN grid rows (every interior factor then has one
+    observed and one free parent): an even-row node copies its LEFT parent
+    (its observed one) with probability ``keep_even``, else uniform, and
+    column 0 of an even row is uniform (rows independent of each other); an
+    odd-row node copies its UP parent (its observed one) with probability
+    ``keep_odd``, else uniform.  So each factor is
+    concentrated on the value its observed parent implies, and its free
+    parent is independent enough of the observed one that most of the free
+    parent's sample points meet training rows (the mean over them stays
+    away from 0 for a 100-factor product)."""
+    rng = np.random.default_rng(seed)
+    n = side * side
+    X = np.zeros((S, n), np.int64)
+    edges = []
+    for r in range(side):
+        for c in range(side):
+            i = r * side + c
+            ps = ([i - 1] if c > 0 else []) + ([i - side] if r > 0 else [])
+            edges += [(f"X{p}", f"X{i}") for p in ps]
+            u = rng.integers(0, d, S)
+            if r % 2 == 0:
+                if c == 0:
+                    X[:, i] = u
+                else:
+                    X[:, i] = np.where(rng.random(S) < keep_even, X[:, i - 1], u)
+            else:
+                X[:, i] = np.where(rng.random(S) < keep_odd, X[:, i - side], u)
+    return X.astype(np.float32), [f"X{i}" for i in range(n)], edges
+
+
 def wide_data(S, seed, k=10, d=2, dy=3):
     """One node Y with k parents P0..P{k-1} (uniform over d levels):
     Y = (sum of the parents + noise) mod dy.  k > 8 is beyond the table
@@ -219,3 +251,18 @@ def continuous_free_data(S, seed):
     X = np.concatenate([R, X2[:, None], X3[:, None]], 1).astype(np.float32)
     cols = ["X0", "X1", "X2", "X3"]
     return X, cols, [("X0", "X3"), ("X1", "X3"), ("X2", "X3")]
+
+
+def grid_rows_evidence(names, Q, seed, d=64, perturb=2):
+    """Evidence for ``grid_rows_data`` networks: every named (even-row) node of
+    query q observes the same level v_q (the value every factor's mass sits on
+    there), and every other query also changes ``perturb`` randomly chosen
+    names to random levels (rows whose products drop by a few factors or
+    vanish)."""
+    rng = np.random.default_rng(seed)
+    v = rng.integers(0, d, Q)
+    ev = {nm: v[:, None].astype(np.float32).copy() for nm in names}
+    for q in range(1, Q, 2):
+        for nm in rng.choice(len(names), size=perturb, replace=False):
+            ev[names[nm]][q, 0] = float(rng.integers(0, d))
+    return ev

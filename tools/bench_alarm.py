@@ -46,6 +46,7 @@ def main():
         out["targets"].append(dict(target=target, factors=len(plan.factors), queries=Q, us_per_call=round(t * 1e6, 2),
                                    queries_per_s=round(Q / t, 1), effective_GBps=round(byt / t / 1e9, 1),
                                    fused_capacity=int(lib.cbn_plan_fused_capacity(plan.handle)),
+                                   plan_flags=int(lib.cbn_plan_flags(plan.handle)),
                                    ))
         print(json.dumps(out["targets"][-1]), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

@@ -82,6 +82,7 @@ def run(keep, noise, prof=False):
                  queries=Q, factors=len(plan.factors), us_per_call=round(t * 1e6, 1), queries_per_s=round(Q / t, 1),
                  effective_GBps=round(byt / t / 1e9, 1), image_MB=round(lib.cbn_plan_table_bytes(plan.handle) / 1e6, 1)
                  if lib else None, fast_path=bool(lib.cbn_plan_max_words(plan.handle)) if lib else None,
+                 plan_flags=int(lib.cbn_plan_flags(plan.handle)) if lib else None,
                  first_call_s=round(plan_s, 2), fit_s=round(fit_s, 1), nonzero_frac=float((pdf > 0).float().mean()),
                  finite_frac=float(torch.isfinite(pdf).float().mean()))
         out["runs"].append(r)
