@@ -76,7 +76,17 @@ struct DirectPlan {
     int* d_qf = nullptr;        // [nq]: factor of each key row
     long long* d_keys = nullptr;  // [nq][Q] observed-parent key of each (factor, query), -1: off-domain
     long long keys_cap = 0;     // elements
+    double query_combos = 0;    // sum over QUERY factors of their free-parent combos (per query and column)
 };
+
+// Work bounds: a direct factor's free-parent mean loops over its
+// F = N^(free parents) combos serially per (query, column) -- the reference
+// materialises Q x F x N pdf values for the same factor (node.py:335-375).
+// The plan takes F <= 2^32 (query-independent factors: F x N <= 2^40, once
+// per plan); a call is refused when Q x N x (sum of its QUERY factors' F)
+// exceeds 2^40 CPD lookups (tens of seconds of GPU time): split the batch.
+constexpr double kDirectCallLookups = 1099511627776.0;  // 2^40
+constexpr long long kDirectMaxCombos = 1LL << 32;
 
 }  // namespace cbn
 
@@ -171,8 +181,8 @@ __global__ void k_cpd_ref_eval(DevCpd c, int n_cols, RefCols rc, const float* __
 
 // x_f[j] for query-independent factors (SCALAR: mean over the N node
 // samples, replicated; SHARED: mean over the N^k parent sample combos)
-__device__ float direct_free_mean(const DevDirect& d, long long base, int N) {
-    float s = 0.f;
+__device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
+    double s = 0.0;  // fp64 sum, one rounding of the mean (see entry_partial, cbn_infer.hip)
     for (long long c = 0; c < d.free_combos; ++c) {
         long long key = base, cc = c;
         bool ok = true;
@@ -186,7 +196,7 @@ __device__ float direct_free_mean(const DevDirect& d, long long base, int N) {
                 key += (long long)(pi < 0 ? 0 : pi) * col.stride;
             }
         }
-        s += ok ? cpd_get(d.cpd, key) : 0.f;
+        s += ok ? (double)cpd_get(d.cpd, key) : 0.0;
     }
     return s;
 }
@@ -199,15 +209,15 @@ __global__ void k_direct_const(const DevDirect* __restrict__ fac, const int* __r
     const DevDirect& d = fac[cfac[r]];
     float x;
     if (d.kind == CBN_FACTOR_SCALAR) {
-        float s = 0.f;
+        double s = 0.0;
         for (int jj = 0; jj < N; ++jj) {
             const int ni = d.node_sample_idx[jj];
-            s += ni >= 0 ? cpd_get(d.cpd, ni) : 0.f;
+            s += ni >= 0 ? (double)cpd_get(d.cpd, ni) : 0.0;
         }
-        x = s / (float)N;
+        x = (float)(s / (double)N);
     } else {
         const int ni = d.node_sample_idx[j];
-        x = ni < 0 ? 0.f : direct_free_mean(d, ni, N) / (float)d.free_combos;
+        x = ni < 0 ? 0.f : (float)(direct_free_mean(d, ni, N) / (double)d.free_combos);
     }
     out[i] = x;
 }
@@ -282,7 +292,7 @@ __global__ void __launch_bounds__(kDThreads) k_query_direct(const DevDirect* __r
                         }
                     }
                 }
-                x = ok ? direct_free_mean(d, base, N) / (float)d.free_combos : 0.f;
+                x = ok ? (float)(direct_free_mean(d, base, N) / (double)d.free_combos) : 0.f;
             }
             acc = acc * x;
         }
@@ -358,6 +368,11 @@ int cbn::direct_run(cbn_plan* plan, int64_t n_queries, const float* const* evide
     DirectPlan* dp = plan->direct;
     if (n_evidence != dp->ns) return set_err(CBN_E_ARG, "plan expects %d evidence columns, got %d", dp->ns, n_evidence);
     if (n_queries <= 0) return set_err(CBN_E_ARG, "cbn_plan_run: direct plans need >= 1 query");
+    if ((double)n_queries * dp->N * dp->query_combos > kDirectCallLookups)
+        return set_err(CBN_E_LIMIT,
+                       "direct plan: %lld queries x %d columns x %.0f free-parent combos = %.3g CPD lookups > 2^40 in one "
+                       "call; split the batch",
+                       (long long)n_queries, dp->N, dp->query_combos, (double)n_queries * dp->N * dp->query_combos);
     if (!out || !max_bits) return set_err(CBN_E_ARG, "cbn_plan_run: null output");
     DEv ev;
     memset(&ev, 0, sizeof(ev));
@@ -449,6 +464,7 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
     const int N = n_samples;
     std::vector<DevDirect> host(n_factors);
     int ns = 0, n_const = 0;
+    double query_combos = 0;
     for (int f = 0; f < n_factors; ++f) {
         const cbn_direct_factor& h = factors[f];
         DevDirect& d = host[f];
@@ -483,16 +499,17 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
                 c.sample_idx = h.parent_sample_idx + (long long)p * N;
                 ++d.n_free;
                 // each (query, column) thread loops over the F free-parent combos
-                // serially; the reference materialises Q x F x N pdf values for
-                // the same factor (node.py:335-375), so beyond 2^20 combos
-                // neither finishes in useful time
-                if (F > (1LL << 20) / N)
-                    return set_err(CBN_E_LIMIT, "factor %d: more than 2^20 free-parent sample combos", f);
+                // serially (work bounds: kDirectMaxCombos / kDirectCallLookups)
+                if (F > kDirectMaxCombos / N)
+                    return set_err(CBN_E_LIMIT, "factor %d: more than 2^32 free-parent sample combos", f);
                 F *= N;
             }
         }
         d.free_combos = F;
         if ((h.kind == CBN_FACTOR_QUERY) != (d.n_obs > 0)) return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
+        if (h.kind == CBN_FACTOR_QUERY) query_combos += (double)F;
+        else if ((double)F * N > kDirectCallLookups)
+            return set_err(CBN_E_LIMIT, "factor %d: %lld free-parent combos x %d columns > 2^40 CPD lookups", f, F, N);
         if (h.kind != CBN_FACTOR_QUERY) d.cidx = n_const++;
     }
     std::vector<int> qf;
@@ -508,6 +525,7 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
     dp->n_const = n_const;
     dp->max_slots = std::min(4 * num_cu(), kMaxSlots);
     dp->nq = (int)qf.size();
+    dp->query_combos = query_combos;
     std::vector<int> cfac;
     for (int f = 0; f < n_factors; ++f)
         if (host[f].kind != CBN_FACTOR_QUERY) cfac.push_back(f);

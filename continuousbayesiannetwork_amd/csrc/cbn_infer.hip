@@ -283,20 +283,25 @@ __global__ void k_cpd_eval(const float* __restrict__ cpd, int n_cols, ColPtrs co
 // domain contribute 0 but still count in F (node.py:291-333 pads with
 // off-domain values).  SCALAR (root) tables hold the mean over the N node
 // samples, replicated over the N columns.  int32 index math throughout
-// (plan_create bounds every table and CPD below 2^31).
-__device__ float entry_partial(const DevFactor& d, int entry, int N, int c0, int c1, int cs) {
+// (plan_create bounds every table and CPD below 2^31).  The sums run in fp64
+// and the mean is rounded to fp32 once: the reference's torch.mean over the
+// meshgrid axes (bayesian_network.py:271-293; node.py:206-284 repeats each
+// observed value N times, so at d = N = 64 one free parent is 4 096 combos)
+// is a cascaded fp32 reduction within a few ulp of the exact mean; a plain
+// fp32 running sum over F terms drifts by up to F/2 ulp.
+__device__ double entry_partial(const DevFactor& d, int entry, int N, int c0, int c1, int cs) {
     if (d.kind == CBN_FACTOR_SCALAR) {
-        float s = 0.f;
+        double s = 0.0;
         for (int j = c0; j < c1; j += cs) {
             const int ni = d.node_sample_idx[j];
-            s += ni >= 0 ? d.cpd[ni] : 0.f;
+            s += ni >= 0 ? (double)d.cpd[ni] : 0.0;
         }
         return s;
     }
     const int row = entry / N;
     const int j = entry - row * N;
     const int ni = d.node_sample_idx[j];
-    if (ni < 0) return 0.f;
+    if (ni < 0) return 0.0;
     int base = ni;  // observed-parent part of the CPD offset (last observed parent fastest)
     int r = row;
     for (int p = d.n_parents - 1; p >= 0; --p) {
@@ -307,7 +312,7 @@ __device__ float entry_partial(const DevFactor& d, int entry, int N, int c0, int
             r = q;
         }
     }
-    float s = 0.f;
+    double s = 0.0;
     for (int c = c0; c < c1; c += cs) {
         int off = base;
         int cc = c;
@@ -321,9 +326,15 @@ __device__ float entry_partial(const DevFactor& d, int entry, int N, int c0, int
                 off += (pi < 0 ? 0 : pi) * d.cpd_stride[p];
             }
         }
-        s += ok ? d.cpd[off] : 0.f;
+        s += ok ? (double)d.cpd[off] : 0.0;
     }
     return s;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
 }
 
 __global__ void __launch_bounds__(kBuildThreads)
@@ -344,11 +355,11 @@ k_build_tables(const DevFactor* __restrict__ fac, const BuildItem* __restrict__ 
         float* tab = image + d.table_off;
         // table rows are RS >= N floats apart (padding spreads LDS banks)
         if (d.wave_mode) {
-            const float s = wave_sum(entry_partial(d, lu, N, lane, F, kWave));
-            if (lane == 0) tab[(lu / N) * RS + lu % N] = s / (float)F;
+            const double s = wave_sum_d(entry_partial(d, lu, N, lane, F, kWave));
+            if (lane == 0) tab[(lu / N) * RS + lu % N] = (float)(s / (double)F);
         } else {
             const int e = lu * kWave + lane;
-            if (e < d.n_entries) tab[(e / N) * RS + e % N] = entry_partial(d, e, N, 0, F, 1) / (float)F;
+            if (e < d.n_entries) tab[(e / N) * RS + e % N] = (float)(entry_partial(d, e, N, 0, F, 1) / (double)F);
         }
     }
 }

@@ -179,3 +179,47 @@ def test_wide_node_many_parents_oracle(gpu):
     np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
     np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
     assert all(f & _native.CBN_PLAN_DIRECT for f in _plan_flags(bn))
+
+
+def test_direct_free_combos_beyond_2_20_and_the_call_bound(gpu):
+    """Direct-plan work bounds: a factor with 6 free 16-level
+    parents at N = 16 has 16^6 = 16.7 M free-parent combos (refused before
+    round 4 by a fixed 2^20 cap) -- it now runs, and its free-parent mean
+    matches an fp64 numpy evaluation of the fitted CPD; a call whose work
+    (queries x columns x combos) exceeds 2^40 CPD lookups is refused with
+    NativeError (CBN_E_LIMIT) before anything launches."""
+    S, k, d = 200_000, 7, 16
+    rng = np.random.default_rng(11)
+    P = rng.integers(0, d, (S, k))
+    Y = (P[:, 0] + P[:, 1] + rng.choice(3, S, p=[0.7, 0.2, 0.1])) % 3
+    X = np.concatenate([P, Y[:, None]], 1).astype(np.float32)
+    cols = [f"P{i}" for i in range(k)] + ["Y"]
+    edges = [(f"P{i}", "Y") for i in range(k)]
+    bn = make_bn(BayesianNetwork, edges, cols, X, device=gpu)
+    ev_np = {"P0": np.array([[3.0], [11.0]], np.float32)}
+    random.seed(5)
+    pdf, dom = bn.infer("Y", _t(ev_np, gpu), N_max=d)
+    out, pts = pdf.cpu().numpy(), dom.cpu().numpy()[0]
+    # fp64 reference of the Y factor: (1/16^6) sum over the present parent
+    # combos p (p0 = e) of P(y | p) = joint / (parent marginal + 1e-10)
+    rows, counts = np.unique(X, axis=0, return_counts=True)
+    probs = counts.astype(np.float32) / np.float32(counts.sum())
+    par = {}
+    for r, pr in zip(rows, probs):
+        key = tuple(r[:k])
+        par[key] = np.float32(par.get(key, np.float32(0)) + pr)
+    x = np.zeros((2, d))
+    for qi, e in enumerate(ev_np["P0"][:, 0]):
+        for r, pr in zip(rows, probs):
+            if r[0] != e:
+                continue
+            for j, y in enumerate(pts):
+                if r[k] == y:
+                    x[qi, j] += float(np.float32(pr / (par[tuple(r[:k])] + np.float32(1e-10))))
+    x /= float(d) ** 6
+    np.testing.assert_allclose(out, x / x.max(), rtol=2e-5, atol=1e-7)
+    assert (out > 0).sum() >= 4
+    # the call bound: 8192 queries x 16 columns x 16^6 combos = 2.2e12 lookups > 2^40
+    big = {"P0": torch.full((8192, 1), 3.0, device=gpu)}
+    with pytest.raises(_native.NativeError, match="split the batch"):
+        bn.infer("Y", big, N_max=d)
