@@ -135,12 +135,6 @@ __device__ __forceinline__ int bsearch_eq(const float* __restrict__ dom, int car
     return (lo < card && dom[lo] == x) ? lo : -1;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
-}
-
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
@@ -1046,10 +1040,12 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // broadcast from LDS) right before gathering the row: no offset buffer, no
 // per-factor evidence reloads.  Same factor order, same products, same
 // outputs as k_query_fast (bit-identical); modes as there.
-constexpr int kColChunk = 40;  // slot loads in flight per lane (ns <= 40 per lane: one round trip)
-constexpr int kColKB = 6;      // factors' rows in flight per gather batch
+// CH: slot loads in flight per lane (all of a lane's slots in one round trip
+// when ceil(ns / L) <= CH): 16 or 40, picked per plan, so a lane does not
+// issue many clamped duplicate loads (configs[4]: 99 slots over 8 lanes = 13)
+constexpr int kColKB = 6;  // factors' rows in flight per gather batch
 
-template <int VPL, bool USE_LDS, int MODE>
+template <int VPL, bool USE_LDS, int MODE, int CH>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats,
              FPtrsT<kFastPtrsSmall> sp, long long Q, long long per, int N, int RS, int L,
@@ -1110,17 +1106,17 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         const bool valid = qq < q1;
         const long long q = valid ? qq : q0;
         if (first) CBN_STAMP(3);
-        // index phase: this lane's slots, kColChunk loads in flight per chunk
-        for (int c0 = 0; c0 < nsl; c0 += kColChunk) {  // (uniform across the wave unless ns % L)
-            float x[kColChunk];
+        // index phase: this lane's slots, CH loads in flight per chunk
+        for (int c0 = 0; c0 < nsl; c0 += CH) {  // (uniform across the wave unless ns % L)
+            float x[CH];
 #pragma unroll
-            for (int k = 0; k < kColChunk; ++k) {
+            for (int k = 0; k < CH; ++k) {
                 int s = l + (c0 + k) * L;
                 s = s < ns ? s : ns - 1;  // unconditional loads: the compiler's waits stay counted
                 x[k] = gload(sptr[s], q);
             }
 #pragma unroll
-            for (int k = 0; k < kColChunk; ++k) {
+            for (int k = 0; k < CH; ++k) {
                 const int s = l + (c0 + k) * L;
                 if (c0 + k < nsl) {
                     const QSlot sr = srec[s];
@@ -1867,7 +1863,8 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
         return;
     }
     if (p->cols) {
-        hipLaunchKernelGGL((k_query_cols<VPL, LDS, MODE>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
+        auto k = (p->ns + L - 1) / L <= 16 ? k_query_cols<VPL, LDS, MODE, 16> : k_query_cols<VPL, LDS, MODE, 40>;
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
                            p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, slot_ptrs(p, ev), Q,
                            (Q + blocks - 1) / blocks, p->N, p->RS, L, p->d_sync, epoch, max_in, n_max, max_out, out,
                            p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
@@ -1880,8 +1877,10 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
 }
 
 template <int VPL, bool LDS, int MODE>
-const void* fast_kernel_fn(int nf, bool cols = false) {
-    if (cols) return reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE>);
+const void* fast_kernel_fn(int nf, bool cols = false, int slots_per_lane = 0) {
+    if (cols)
+        return slots_per_lane <= 16 ? reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE, 16>)
+                                    : reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE, 40>);
     return nf * kFastObs <= kFastPtrsSmall ? reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>)
                                            : reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>);
 }
@@ -1892,7 +1891,9 @@ void allow_fast_lds(int bytes) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE, 16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_cols<VPL, LDS, MODE, 40>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
@@ -2480,11 +2481,12 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 allow_fast_lds<1, false, kModeFused>(kLdsBudget);
                 allow_fast_lds<2, false, kModeFused>(kLdsBudget);
                 int nb = 0;
+                const int spl = (ns + Lf - 1) / Lf;  // k_query_cols: slots per lane
                 const void* fn = P->staged ? reinterpret_cast<const void*>(&k_query_staged<kModeFused>)
-                                 : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors, P->cols)
-                                                          : fast_kernel_fn<1, true, kModeFused>(n_factors, P->cols))
-                                              : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors, P->cols)
-                                                          : fast_kernel_fn<1, false, kModeFused>(n_factors, P->cols));
+                                 : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors, P->cols, spl)
+                                                          : fast_kernel_fn<1, true, kModeFused>(n_factors, P->cols, spl))
+                                              : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors, P->cols, spl)
+                                                          : fast_kernel_fn<1, false, kModeFused>(n_factors, P->cols, spl));
                 const size_t lb = P->staged ? P->staged_lds_bytes : P->fast_lds_bytes;
                 if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kQueryThreads, lb) == hipSuccess && nb >= 1)
                     P->fused_ok = true;
