@@ -7,13 +7,14 @@
 //   hipcc --offload-arch=gfx950 -O3 -o tools/probes/valu_rate tools/probes/valu_rate.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <algorithm>
 #include <vector>
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kIters = 2048;
 
 template <int OP>
-__global__ void __launch_bounds__(256) k(unsigned long long* cyc, float* sink, float c) {
+__global__ void __launch_bounds__(1024) k(unsigned long long* cyc, float* sink, float c) {
     float a[8];
     f2 b[8];
 #pragma unroll
@@ -41,7 +42,7 @@ __global__ void __launch_bounds__(256) k(unsigned long long* cyc, float* sink, f
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) / 64] = t1 - t0;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += a[j] + b[j].x + b[j].y;
@@ -56,26 +57,33 @@ void run(const char* name, int cus) {
     hipMalloc(&dcyc, sizeof(unsigned long long) * maxb * 4);
     hipMalloc(&sink, 1024 * 4);
     printf("%-10s", name);
-    for (int w : {1, 2, 4, 7, 8}) {
-        const int blocks = cus * w;  // 256 threads = one wave per SIMD per block
-        hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, dcyc, sink, 0.999f);
+    for (int w : {1, 2, 4, 8}) {
+        // one block of 256 w threads per CU (w <= 4), two of 1024 for w = 8:
+        // every wave of a CU is dispatched at once
+        const int per = w <= 4 ? w : 4;
+        const int blocks = cus * (w / per);
+        const int threads = 256 * per;
+        hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(threads), 0, 0, dcyc, sink, 0.999f);
         hipEvent_t e0, e1;
         hipEventCreate(&e0);
         hipEventCreate(&e1);
         hipEventRecord(e0);
-        hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(256), 0, 0, dcyc, sink, 0.999f);
+        hipLaunchKernelGGL(k<OP>, dim3(blocks), dim3(threads), 0, 0, dcyc, sink, 0.999f);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms = 0;
         hipEventElapsedTime(&ms, e0, e1);
-        std::vector<unsigned long long> h(blocks * 4);
-        hipMemcpy(h.data(), dcyc, sizeof(unsigned long long) * blocks * 4, hipMemcpyDeviceToHost);
-        double avg = 0;
-        for (auto v : h) avg += (double)v;
+        const int nw = blocks * threads / 64;
+        std::vector<unsigned long long> h(nw);
+        hipMemcpy(h.data(), dcyc, sizeof(unsigned long long) * nw, hipMemcpyDeviceToHost);
+        double avg = 0, mx = 0;
+        for (auto v : h) { avg += (double)v; mx = std::max(mx, (double)v); }
         avg /= h.size();
         const double ins = (double)kIters * 8;
-        // per SIMD: w waves each issuing `ins` instructions over ~avg cycles
-        printf("  w=%d %.2f cyc/instr (wave %.0f cyc, kernel %.1f us)", w, avg / (w * ins), avg, ms * 1e3);
+        // per SIMD: w co-resident waves each issuing `ins` instructions over ~avg cycles;
+        // clock = the longest wave's cycles / the kernel's time (co-residency check)
+        printf("  w=%d %.2f cyc/instr (wave avg %.0f max %.0f cyc, kernel %.1f us, %.2f GHz)", w, avg / (w * ins), avg,
+               mx, ms * 1e3, mx / (ms * 1e6));
     }
     printf("\n");
     hipFree(dcyc);

@@ -23,7 +23,7 @@ import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OURS = ("k_query_staged", "k_query_fast", "k_query<", "k_build_tables", "k_cpd_", "k_scale", "k_param")
+OURS = ("k_query_staged", "k_query_fast", "k_query_cols", "k_query<", "k_build_tables", "k_cpd_", "k_scale", "k_param")
 
 
 def short_name(name: str) -> str:
