@@ -407,6 +407,96 @@ at::Tensor check_out(py::object& out_obj, int64_t n, int64_t n_samples, int64_t 
     return out;
 }
 
+// One cached (target, evidence keys, N) of InferenceEngine.infer, callable
+// straight from BayesianNetwork.infer (round 4): the caller's dict is matched
+// against the key tuple it was built for by walking the dict once in
+// insertion order (key identity, else string equality) -- no key tuple built
+// and hashed, no engine dict lookup, no per-call Python frames -- the slot
+// columns are picked by position during that walk, the output is allocated
+// and the plan launched; returns (out, target domain view), or None when the
+// dict does not match / a fast check fails (the engine's general path then
+// runs: conversions, the reference's errors), or the C ABI's error code.
+// Only deterministic plans with their tables built (flags fixed at
+// construction) get a runner.
+class Runner {
+  public:
+    Runner(uintptr_t fn, uintptr_t plan, py::tuple keys, py::tuple slots, int64_t device_index, int64_t n_samples,
+           bool target_observed, uintptr_t max_ptr, int32_t flags, py::object target_domain)
+        : run_(reinterpret_cast<run_fn>(fn)), plan_(reinterpret_cast<void*>(plan)), keys_(keys), dev_(device_index),
+          n_samples_(n_samples), target_observed_(target_observed), max_ptr_(reinterpret_cast<unsigned*>(max_ptr)),
+          flags_(flags), tdom_(THPVariable_Unpack(target_domain.ptr())) {
+        const Py_ssize_t nk = PyTuple_GET_SIZE(keys.ptr());
+        for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(slots.ptr()); ++i) {
+            Py_ssize_t pos = -1;
+            for (Py_ssize_t j = 0; j < nk && pos < 0; ++j)
+                if (PyObject_RichCompareBool(PyTuple_GET_ITEM(keys.ptr(), j), PyTuple_GET_ITEM(slots.ptr(), i), Py_EQ) == 1)
+                    pos = j;
+            if (pos < 0) throw std::invalid_argument("Runner: slot key not among the evidence keys");
+            slot_pos_.push_back(pos);
+        }
+        vals_.resize(nk);
+        ptrs_.resize(std::max<size_t>(1, slot_pos_.size()));
+    }
+
+    py::object call(py::handle evidence, py::object out_obj) {
+        PyObject* d = evidence.ptr();
+        if (!PyDict_CheckExact(d)) return py::none();
+        const Py_ssize_t nk = PyTuple_GET_SIZE(keys_.ptr());
+        if (PyDict_GET_SIZE(d) != nk) return py::none();
+        Py_ssize_t it = 0, j = 0;
+        PyObject *k, *v;
+        while (PyDict_Next(d, &it, &k, &v)) {
+            PyObject* want = PyTuple_GET_ITEM(keys_.ptr(), j);
+            if (k != want && PyObject_RichCompareBool(k, want, Py_EQ) != 1) return py::none();
+            vals_[j++] = v;
+        }
+        int64_t n = 1;
+        if (nk > 0) {
+            PyObject* f = vals_[0];
+            if (!THPVariable_Check(f)) return py::none();
+            const at::Tensor& t = THPVariable_Unpack(f);
+            if (t.dim() < 1) return py::none();
+            n = t.size(0);
+        }
+        if (n == 0 || (!target_observed_ && n != 1)) return py::none();
+        for (size_t i = 0; i < slot_pos_.size(); ++i) {
+            PyObject* x = vals_[slot_pos_[i]];
+            if (!THPVariable_Check(x)) return py::none();
+            const at::Tensor& t = THPVariable_Unpack(x);
+            if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev_ || t.dim() != 2 ||
+                t.size(0) != n || !t.is_contiguous())
+                return py::none();
+            ptrs_[i] = static_cast<const float*>(t.data_ptr());
+        }
+        if (c10::hip::current_device() != dev_) return py::none();
+        at::Tensor out = check_out(out_obj, n, n_samples_, dev_);
+        const hipStream_t s = c10::hip::getCurrentHIPStream(dev_).stream();
+        const int rc = run_(plan_, n, ptrs_.data(), (int32_t)slot_pos_.size(), max_ptr_,
+                            static_cast<float*>(out.data_ptr()), flags_, s);
+        if (rc) return py::int_(rc);
+        const int64_t tn = target_observed_ ? n : 1;
+        if (tn != tdom_n_) {
+            tdom_view_ = tdom_.unsqueeze(0).expand({tn, -1});
+            tdom_n_ = tn;
+        }
+        return py::make_tuple(out, tdom_view_);
+    }
+
+  private:
+    run_fn run_;
+    void* plan_;
+    py::tuple keys_;
+    int64_t dev_, n_samples_;
+    bool target_observed_;
+    unsigned* max_ptr_;
+    int32_t flags_;
+    at::Tensor tdom_, tdom_view_;
+    int64_t tdom_n_ = -1;
+    std::vector<Py_ssize_t> slot_pos_;
+    std::vector<PyObject*> vals_;
+    std::vector<const float*> ptrs_;
+};
+
 class Stepper {
   public:
     Stepper(uintptr_t run_addr, uintptr_t scale_batch_addr, uintptr_t plan, py::tuple slots, py::object first,
@@ -1069,6 +1159,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("nccl_unique_id", &nccl_unique_id);
     m.def("nccl_comm_init", &nccl_comm_init);
     m.def("nccl_comm_destroy", &nccl_comm_destroy);
+    py::class_<Runner>(m, "Runner")
+        .def(py::init<uintptr_t, uintptr_t, py::tuple, py::tuple, int64_t, int64_t, bool, uintptr_t, int32_t,
+                      py::object>())
+        .def("__call__", &Runner::call, py::arg("evidence"), py::arg("out") = py::none());
     py::class_<Stepper>(m, "Stepper")
         .def(py::init<uintptr_t, uintptr_t, uintptr_t, py::tuple, py::object, int64_t, int64_t, bool, int64_t, int,
                       uintptr_t, int, int>())

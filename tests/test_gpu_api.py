@@ -194,3 +194,70 @@ def test_variable_elimination_query_matches_reference_golden(gpu):
                     else ve.infer(m["target"], ev, None, N_max=m["N_max"]))
         np.testing.assert_array_equal(dom.cpu().numpy(), g["domain"])
         np.testing.assert_allclose(pdf.cpu().numpy(), g["pdf"], rtol=RTOL, atol=ATOL)
+
+
+def test_native_runner_path_matches_and_falls_back(gpu):
+    """The native Runner (csrc/host_fast.cpp) serves repeat calls of the last
+    (target, evidence keys, N): same outputs as the general path bit for bit;
+    other key orders, extra keys, a float64 column, a CPU column, a missing
+    key, evidence=None, out=, a timed call and a refit all take the general
+    path with the reference's behaviour, and the runner comes back after."""
+    data, cols, edges = chain_data(8, 8, 5000, 4, stay=0.7)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    names = [c for c in cols if c != "X7"]
+    ev = _t(sample_evidence(data, cols, names, 777, 2), gpu)
+    eng = bn.engine
+    a, da = bn.infer("X7", ev, N_max=8)  # general path; sets the runner
+    assert eng._runner is not None and eng._runner[:2] == ("X7", 8)
+    b, db = bn.infer("X7", dict(ev), N_max=8)  # runner path (a new dict, same keys)
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    assert torch.equal(da, db) and db.shape == (777, 8)
+    ref, _ = OracleBN(edges, cols, data).infer("X7", {k: v.cpu().numpy() for k, v in ev.items()}, 8)
+    np.testing.assert_allclose(b.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    # another key order: the general path (its own fast path), same values
+    rev = {k: ev[k] for k in reversed(list(ev))}
+    c, _ = bn.infer("X7", rev, N_max=8)
+    np.testing.assert_array_equal(c.cpu().numpy(), a.cpu().numpy())
+    # a float64 column / a CPU column: converted by the general path
+    ev64 = dict(ev)
+    ev64["X6"] = ev["X6"].double()
+    np.testing.assert_array_equal(bn.infer("X7", ev64, N_max=8)[0].cpu().numpy(), a.cpu().numpy())
+    evc = dict(ev)
+    evc["X3"] = ev["X3"].cpu()
+    np.testing.assert_allclose(bn.infer("X7", evc, N_max=8)[0].cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    # the reference's errors still raise
+    with pytest.raises(AttributeError):
+        bn.infer("X7", None, N_max=8)
+    bad = dict(ev)
+    bad["X6"] = ev["X6"][:5]
+    with pytest.raises(AssertionError):
+        bn.infer("X7", bad, N_max=8)
+    # out= through the runner
+    bn.infer("X7", ev, N_max=8)
+    out = torch.empty((777, 8), device=gpu)
+    r, _ = eng.infer("X7", dict(ev), 8, out=out)
+    assert r.data_ptr() == out.data_ptr()
+    np.testing.assert_array_equal(out.cpu().numpy(), a.cpu().numpy())
+    # changing a per-call flag drops the runner
+    eng.timed = True
+    assert eng._runner is None
+    np.testing.assert_array_equal(bn.infer("X7", ev, N_max=8)[0].cpu().numpy(), a.cpu().numpy())
+    eng.timed = False
+    eng.timing()
+    bn.infer("X7", ev, N_max=8)
+    assert eng._runner is not None
+    # a refit drops it with the plans: the next call follows the new CPD
+    from oracle.ref_infer import OracleNode
+
+    data2, _, _ = chain_data(8, 8, 5000, 9, stay=0.3)
+    y, x = data2[:, cols.index("X7")], data2[:, cols.index("X6")][None, :]
+    bn.nodes_obj["X7"].fit(torch.tensor(y, device=gpu), torch.tensor(x, device=gpu))
+    got, _ = bn.infer("X7", ev, N_max=8)
+    ora = OracleBN(edges, cols, data)
+    node = OracleNode("X7", ["X6"])
+    node.fit(y, x)
+    ora.nodes["X7"] = node
+    ref2, _ = ora.infer("X7", {k: v.cpu().numpy() for k, v in ev.items()}, 8)
+    np.testing.assert_allclose(got.cpu().numpy(), ref2, rtol=RTOL, atol=ATOL)
+    got2, _ = bn.infer("X7", dict(ev), N_max=8)  # the rebuilt plan's runner
+    np.testing.assert_array_equal(got2.cpu().numpy(), got.cpu().numpy())
