@@ -207,8 +207,11 @@ def test_native_runner_path_matches_and_falls_back(gpu):
     names = [c for c in cols if c != "X7"]
     ev = _t(sample_evidence(data, cols, names, 777, 2), gpu)
     eng = bn.engine
-    a, da = bn.infer("X7", ev, N_max=8)  # general path; sets the runner
+    a, da = bn.infer("X7", ev, N_max=8)  # plans + caches the fast path
+    assert eng._runner is None
+    a2, _ = bn.infer("X7", ev, N_max=8)  # cached fast path; sets the runner
     assert eng._runner is not None and eng._runner[:2] == ("X7", 8)
+    np.testing.assert_array_equal(a.cpu().numpy(), a2.cpu().numpy())
     b, db = bn.infer("X7", dict(ev), N_max=8)  # runner path (a new dict, same keys)
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     assert torch.equal(da, db) and db.shape == (777, 8)
@@ -244,7 +247,7 @@ def test_native_runner_path_matches_and_falls_back(gpu):
     np.testing.assert_array_equal(bn.infer("X7", ev, N_max=8)[0].cpu().numpy(), a.cpu().numpy())
     eng.timed = False
     eng.timing()
-    bn.infer("X7", ev, N_max=8)
+    bn.infer("X7", ev, N_max=8)  # cached fast path again: the runner is back
     assert eng._runner is not None
     # a refit drops it with the plans: the next call follows the new CPD
     from oracle.ref_infer import OracleNode

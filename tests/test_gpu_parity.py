@@ -676,3 +676,47 @@ def test_raw_launch_with_folded_scale(Q0, Q1, gpu):
     np.testing.assert_array_equal(out1.cpu().numpy(), rows1.cpu().numpy())
     np.testing.assert_array_equal(words.cpu().numpy(), w1.cpu().numpy())
     np.testing.assert_array_equal(rows0.cpu().numpy(), ref0.cpu().numpy())
+
+
+FREE_PARENT_GRIDS = ["grid10_d64_dense_ref", "grid10_d64_rows_ref", "grid10_d64_rows_x99_ref"]
+
+
+@pytest.mark.parametrize("name", FREE_PARENT_GRIDS)
+@pytest.mark.parametrize("direct", [False, True], ids=["tables", "direct"])
+def test_grid_free_parent_means_match_reference(name, direct, gpu):
+    """Free-parent means at configs[4]'s size, pinned by the REFERENCE's own
+    infer (tests/golden/make_golden_full.py): d = N = 64 grids with evidence
+    on the even grid rows only, so every factor with a parent in an odd row
+    averages over that parent's 64 sample points (4 096 meshgrid combos in
+    the reference, node.py:206-284 -> bayesian_network.py:271-293) --
+    k_build_tables' table rows, and (``direct``) k_query_direct's per-(query,
+    column) means.  Cases: the full 100-factor X99 plan (86 factors with a
+    free parent, 4 queries), 32 queries on X33 (10 free-parent factors), and
+    a dense case (X21, ~24 % of the marginals nonzero)."""
+    import json
+    import os
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_golden_full import CASES, digest, make_case
+
+    z = np.load(os.path.join(here, "golden", name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    data, cols, edges, ev_np = make_case(CASES[name])
+    assert digest([data]) == meta["data_sha256"]
+    assert digest([ev_np[k] for k in sorted(ev_np)]) == meta["evidence_sha256"]
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    bn.engine.force_direct = direct
+    random.seed(0)
+    pdf, dom = bn.infer(meta["target"], _t(ev_np, gpu), N_max=meta["N_max"])
+    out = pdf.cpu().numpy()
+    ref = z["pdf"]
+    assert list(z["rows"]) == list(range(meta["Q"]))
+    np.testing.assert_array_equal(dom.cpu().numpy()[:1], z["domain"][:1])
+    np.testing.assert_array_equal(out > 0, ref > 0)  # same support
+    np.testing.assert_allclose(out, ref, rtol=RTOL, atol=ATOL)
+    nz = ref > 0
+    assert np.isfinite(ref).all() and nz.any()
+    # relative agreement on the nonzero marginals themselves (atol aside)
+    assert float(np.max(np.abs(out[nz] - ref[nz]) / ref[nz])) <= RTOL

@@ -100,3 +100,30 @@ def test_grid_oracle_fixture_matches_reference_run():
     assert (rdom == rdom[:1]).all() and (z["domain"] == rdom[:1]).all()
     assert np.isfinite(ref).all() and ref.max() == 1.0
     np.testing.assert_allclose(z["pdf"], ref, rtol=RTOL, atol=ATOL)
+
+
+def test_free_parent_grid_fixtures_regenerate_their_inputs():
+    """The free-parent grid fixtures' data and evidence come back bit for bit
+    from the committed generators (tests/helpers.py grid_rows_data /
+    grid_rows_evidence / grid_data), so the GPU tests rebuild exactly the
+    reference's inputs; their outputs are finite and non-degenerate."""
+    import json
+    import os
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_golden_full import CASES, digest, make_case
+
+    for name in ("grid10_d64_dense_ref", "grid10_d64_rows_ref", "grid10_d64_rows_x99_ref"):
+        z = np.load(os.path.join(here, "golden", name + ".npz"))
+        meta = json.loads(str(z["meta"]))
+        data, cols, edges, ev = make_case(CASES[name])
+        assert digest([data]) == meta["data_sha256"], name
+        assert digest([ev[k] for k in sorted(ev)]) == meta["evidence_sha256"], name
+        assert sorted(ev) == meta["evidence_columns"]
+        assert all((int(k[1:]) // 10) % 2 == 0 for k in ev)  # even grid rows only
+        pdf = z["pdf"]
+        assert np.isfinite(pdf).all() and pdf.max() == 1.0
+        if name == "grid10_d64_dense_ref":
+            assert (pdf > 0).mean() >= 0.2

@@ -5,7 +5,9 @@ a few host-side variants:
   base      -- bench.py's loop as is
   gcoff     -- gc disabled inside the timed region
   spin      -- poll the end event (busy) before torch.cuda.synchronize()
-  pin       -- main thread pinned to one core
+  busy      -- a spin kernel holds the stream before the timed steps (every
+               launch then enqueues behind queued work: launch cost on a busy
+               vs an idle queue)
 Prints one JSON line per variant: per-step host us, region events us, sync us."""
 import gc
 import json
@@ -45,7 +47,7 @@ def main():
         return bn.infer("X19", ev, N_max=32)
 
     random.seed(0)
-    for variant in ("base", "gcoff", "spin", "pin", "base", "spin"):
+    for variant in ("base", "busy", "spin", "base", "busy", "spin"):
         for _ in range(W):
             step()
         torch.cuda.synchronize()
@@ -55,6 +57,8 @@ def main():
             os.sched_setaffinity(0, {min(aff)})
         if variant == "gcoff":
             gc.disable()
+        if variant == "busy":  # the launch queue starts non-empty: a ~300 us spin kernel ahead of the steps
+            torch.cuda._sleep(600_000)
         ts = []
         t0 = time.perf_counter()
         ev0.record()
