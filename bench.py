@@ -409,11 +409,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()  # the library launches on torch's current stream: these events bracket every launch
+    per_step_events = not sharded and not fused
     for i in range(K):
         # two-launch path: HIP events recorded inside the library around the
-        # passes of every 8th step (the sharded step is timed over the region:
-        # per-step event records cost it ~3 us per step)
-        bn.engine.timed = not sharded and not fused and i % 8 == 7
+        # passes of every 8th step (the sharded step and the fused launch are
+        # timed over the region: per-step event records cost ~3 us per step)
+        if per_step_events:
+            bn.engine.timed = i % 8 == 7
         step()
     t_enq = time.perf_counter()  # host done enqueueing the K steps
     stepper.wait()

@@ -288,8 +288,9 @@ class InferenceEngine:
 
     @timed.setter
     def timed(self, v):
+        if getattr(self, "_timed", None) != v:
+            self._runner = None
         self._timed = v
-        self._runner = None
 
     @property
     def fused(self):
@@ -297,8 +298,9 @@ class InferenceEngine:
 
     @fused.setter
     def fused(self, v):
+        if getattr(self, "_fused", None) != v:
+            self._runner = None
         self._fused = v
-        self._runner = None
 
     @property
     def cache_tables(self):
@@ -306,8 +308,9 @@ class InferenceEngine:
 
     @cache_tables.setter
     def cache_tables(self, v):
+        if getattr(self, "_cache_tables", None) != v:
+            self._runner = None
         self._cache_tables = v
-        self._runner = None
 
     def invalidate(self):
         self._runner = None
