@@ -16,7 +16,8 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 from . import _buildstamp
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(_HERE, "libcbn_amd.so")  # override: diagnostic builds
+_DEFAULT_LIB = os.path.join(_HERE, "libcbn_amd.so")
+LIB_PATH = os.environ.get("CBN_LIB_PATH") or _DEFAULT_LIB  # override: diagnostic builds
 
 ABI_VERSION = 4
 CBN_MAX_PARENTS = 8
@@ -196,7 +197,7 @@ def load() -> ctypes.CDLL:
             raise NativeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(no CPU fallback exists for the HIP inference path)")
-        if not os.environ.get("CBN_LIB_PATH"):  # (diagnostic variant builds carry no stamp)
+        if LIB_PATH == _DEFAULT_LIB:  # (diagnostic variant builds under tools/ carry no stamp)
             _check_stamp(LIB_PATH, _buildstamp.lib_digest())
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
