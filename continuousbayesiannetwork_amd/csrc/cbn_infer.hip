@@ -567,7 +567,6 @@ struct alignas(16) FastRec {
 };
 constexpr int kDenseBit = 1 << 30;
 constexpr int kRecFloats = sizeof(FastRec) / 4;
-static_assert(sizeof(FastRec) == 64, "k_query_cols reads a FastRec as four int4");
 
 // Fast path: the L = N / (4 VPL) lanes of one query (a power of two dividing
 // 64, so a query never straddles waves) split its factors: lane l loads the
@@ -1080,6 +1079,7 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     __syncthreads();
     CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
+    const FastRec* rec = reinterpret_cast<const FastRec*>(simg + lrec);
     const QSlot* srec = reinterpret_cast<const QSlot*>(simg + lrec + nf * kRecFloats);
 
     float maxv = 1.f;
@@ -1141,29 +1141,22 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         // row offsets of factors [f0, f0 + kColKB) from the slots' indices
         // (records and indices are LDS reads); software-pipelined: the next
         // batch's offsets are formed while this batch's row gathers fly
-        // (the records are wave-uniform: scalar loads from the image into
-        // SGPRs -- no LDS instructions, no VGPRs -- FastRec = 4 int4:
-        // {table_off, n_obs, card0, card1} {card2, card3, dom..} {dom.., slot0, slot1} {slot2, slot3, pad})
         auto offsets = [&](int f0, int (&oo)[kColKB]) {
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
                 const int f = f0 + k;
                 int o = -1;
                 if (f < nf) {
-                    const float* rp = gimage + rec_off + f * kRecFloats;
-                    const int4 r0 = sload_int4(rp), r1 = sload_int4(rp + 4), r2 = sload_int4(rp + 8),
-                               r3 = sload_int4(rp + 12);
-                    const int card[kFastObs] = {r0.z, r0.w, r1.x, r1.y};
-                    const int slot[kFastObs] = {r2.z, r2.w, r3.x, r3.y};
-                    o = r0.x;
+                    const FastRec& r = rec[f];
+                    o = r.table_off;
                     int row = 0;
                     bool ok = true;
 #pragma unroll
                     for (int p = 0; p < kFastObs; ++p) {
-                        if (p < r0.y) {
-                            const int i = sidx[slot[p] * QB + ql];
+                        if (p < r.n_obs) {
+                            const int i = sidx[r.slot[p] * QB + ql];
                             ok &= i >= 0;
-                            row = row * (card[p] & (kDenseBit - 1)) + (i < 0 ? 0 : i);
+                            row = row * (r.card[p] & (kDenseBit - 1)) + (i < 0 ? 0 : i);
                         }
                     }
                     o = ok ? o + row * RS : -1;
