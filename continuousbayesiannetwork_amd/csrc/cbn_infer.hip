@@ -1138,10 +1138,8 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         if (first) CBN_STAMP(4);
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-        // row offsets of factors [f0, f0 + kColKB) from the slots' indices
-        // (records and indices are LDS reads); software-pipelined: the next
-        // batch's offsets are formed while this batch's row gathers fly
-        auto offsets = [&](int f0, int (&oo)[kColKB]) {
+        for (int f0 = 0; f0 < nf; f0 += kColKB) {
+            int oo[kColKB];
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
                 const int f = f0 + k;
@@ -1163,10 +1161,6 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 }
                 oo[k] = o;
             }
-        };
-        int oo[kColKB];
-        offsets(0, oo);
-        for (int f0 = 0; f0 < nf; f0 += kColKB) {
             float4 t[kColKB][VPL];
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
@@ -1178,8 +1172,6 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 #pragma unroll
                 for (int v = 0; v < VPL; ++v) t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            int on[kColKB];
-            offsets(f0 + kColKB, on);  // (all -1 past the last factor)
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
                 if (f0 + k < nf) {
@@ -1192,8 +1184,6 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                     }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < kColKB; ++k) oo[k] = on[k];
         }
         if (first) CBN_STAMP(5);
         if (valid) {
