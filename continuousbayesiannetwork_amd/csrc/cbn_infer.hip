@@ -2445,9 +2445,12 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             P->fast_lds_bytes =
                 ((P->use_lds ? img_bytes : (size_t)P->lds_tab_floats * 4 + (size_t)n_factors * kRecFloats * 4) + side +
                  15) & ~size_t(15);
-            // column-staged kernel (k_query_cols): non-paired plans whose slot
-            // indices fit int16 and whose per-slot index buffer fits LDS
-            if (!P->staged && !P->paired && ns <= kFastPtrsSmall && !getenv("CBN_NO_COLS")) {
+            // column-staged kernel (k_query_cols): non-paired plans of <= 2
+            // lanes per query (N <= 16) whose slot indices fit int16 and whose
+            // per-slot index buffer fits LDS.  With more lanes per query every
+            // lane re-forms every factor's offset: the configs[4] grid (L = 8)
+            // ran 459 -> 534 us at 262 144 queries (profiles/r04_cols_ab.json)
+            if (!P->staged && !P->paired && Lf <= 2 && ns <= kFastPtrsSmall && !getenv("CBN_NO_COLS")) {
                 bool ok_c = true;
                 for (int sl = 0; sl < ns; ++sl) ok_c = ok_c && slot_card[sl] <= 32767;
                 for (int f = 0; f < n_factors && ok_c; ++f)
