@@ -96,6 +96,8 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=64,
                     help="distinct evidence batches cycled through (64 x 5 MB > the 256 MB Infinity Cache, so "
                          "evidence is read from HBM, not from a cache warmed by the previous step)")
+    ap.add_argument("--no-touch", action="store_true",
+                    help="do not read every evidence batch once on the device during setup (first-touch A/B)")
     ap.add_argument("--two-pass", action="store_true", help="force the two-launch (max, write) path")
     ap.add_argument("--sharded", action="store_true",
                     help="run the N>1 step (raw launch + RCCL all-reduce + scale, pipelined) even at N=1")
@@ -346,6 +348,15 @@ def main():
     for b in range(max(1, a.batches)):
         perm = torch.randperm(Q, generator=g) if b else torch.arange(Q)
         batches.append({k: v[perm].contiguous().to(dev) for k, v in base.items()})
+    if not a.no_touch:
+        # setup, untimed: read every uploaded column once on the device (the
+        # inputs are resident in HBM AND mapped when the timed region starts;
+        # a batch's first read otherwise pays its page-table walks inside a step)
+        chk = torch.zeros((), device=dev)
+        for ev in batches:
+            for v in ev.values():
+                chk += v.sum()
+        torch.cuda.synchronize()
     it = [0]
     # N>1: one raw launch per step on the compute stream; the all-reduce(MAX)
     # of the block max words + the in-place scale (+ the all-gather) run on a
