@@ -420,8 +420,10 @@ def main():
     if sharded:
         barrier("before the timed region")
     torch.cuda.synchronize()
+    # the library launches on torch's current stream: these events bracket
+    # every launch (instrumentation, recorded before the host clock starts)
+    ev0.record()
     t0 = time.perf_counter()
-    ev0.record()  # the library launches on torch's current stream: these events bracket every launch
     per_step_events = not sharded and not fused
     for i in range(K):
         # two-launch path: HIP events recorded inside the library around the
