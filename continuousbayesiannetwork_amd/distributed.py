@@ -337,6 +337,7 @@ class ShardedStepper:
         self._serial = False
         self._folded = False
         self._epoch = None  # engine.epoch the native stepper's plan handle belongs to
+        self._hot_counts = {}  # total_rows -> every rank's rows (gather=True step ring), for the hot path
 
     def _setup(self, evidence_shard) -> bool:
         import ctypes
@@ -399,17 +400,25 @@ class ShardedStepper:
         self.n_steps += 1
         if self.watchdog is not None:
             self.watchdog.beat(step=self.n_steps)
-        if c is not None and GENERATION[0] == eng._gen and eng.epoch == self._epoch and self._folded:
-            # hot path (rank-local, folded): one native call
+        if c is not None and GENERATION[0] == eng._gen and eng.epoch == self._epoch:
+            # hot path: one native call (folded ring, or the step ring with the
+            # gather counts of this total_rows, cached)
             fp = self._fp
-            res = c.step(evidence_shard, out, eng._flags(fp.plan) | _RAW)
+            if self._folded:
+                res = c.step(evidence_shard, out, eng._flags(fp.plan) | _RAW)
+            else:
+                counts = self._hot_counts.get(total_rows, False) if self.gather else None
+                if counts is False:
+                    return self._step_slow(evidence_shard, out, total_rows)
+                res = c.step(evidence_shard, out, eng._flags(fp.plan) | _RAW, counts)
             if type(res) is torch.Tensor:
                 tdom = fp.tdom.get(res.shape[0])
                 return res, (tdom if tdom is not None else self._tdom(fp, res.shape[0]))
             if res is not None:  # an error code: the step is enqueued (zero words), report it
                 from . import _native
 
-                _native.check(res, "cbn_plan_run_fold")
+                _native.check(res, "cbn_plan_run_fold" if self._folded else "cbn_plan_run(raw)")
+            # None: evidence the native checks reject -> the slow path converts (same ring)
         return self._step_slow(evidence_shard, out, total_rows)
 
     @staticmethod
@@ -437,6 +446,10 @@ class ShardedStepper:
         n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
         flags = eng.raw_flags(fp.plan)
         counts = None if self._folded else self._counts(n, total_rows)
+        if self.gather and not self._folded and (total_rows is not None or self.world == 1):
+            # the counts depend on total_rows only (world 1: on n, so not cached)
+            if total_rows is not None:
+                self._hot_counts[total_rows] = counts
 
         def native_step(ev):
             return self._c.step(ev, out, flags) if self._folded else self._c.step(ev, out, flags, counts)
