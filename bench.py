@@ -454,6 +454,10 @@ def main():
               "outside_region_us": round((t_sync - t0) * 1e6 - region_us, 2)}
     if sharded:
         timing["barrier_us"] = round((t1 - t_sync) * 1e6, 2)
+        c = getattr(stepper, "_c", None)
+        if c is not None and hasattr(c, "host_timing"):  # the step ring's native phases (us per step)
+            ht = c.host_timing()
+            timing["stepper_host_us"] = {"gather_alloc": round(ht[0], 2), "launch_and_exchange": round(ht[1], 2)}
 
     roofline = None
     ntimed, tmax_ms, twrite_ms = bn.engine.timing() if not sharded else (0, 0.0, 0.0)
