@@ -5,6 +5,8 @@ a few host-side variants:
   base      -- bench.py's loop as is
   gcoff     -- gc disabled inside the timed region
   spin      -- poll the end event (busy) before torch.cuda.synchronize()
+  prespin   -- the host polls the warmup's completion before the opening
+               synchronize (it never sleeps in a blocking wait)
   busy      -- a spin kernel holds the stream before the timed steps (every
                launch then enqueues behind queued work: launch cost on a busy
                vs an idle queue)
@@ -47,9 +49,14 @@ def main():
         return bn.infer("X19", ev, N_max=32)
 
     random.seed(0)
-    for variant in ("base", "busy", "spin", "base", "busy", "spin"):
+    for variant in ("base", "prespin", "base", "prespin", "base", "prespin"):
         for _ in range(W):
             step()
+        if variant == "prespin":  # poll the warmup's completion (the host never sleeps), then synchronize
+            ew = torch.cuda.Event()
+            ew.record()
+            while not ew.query():
+                pass
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         aff = os.sched_getaffinity(0)
@@ -60,8 +67,8 @@ def main():
         if variant == "busy":  # the launch queue starts non-empty: a ~300 us spin kernel ahead of the steps
             torch.cuda._sleep(600_000)
         ts = []
-        t0 = time.perf_counter()
         ev0.record()
+        t0 = time.perf_counter()
         for _ in range(K):
             step()
             ts.append(time.perf_counter())
