@@ -421,6 +421,13 @@ def main():
         wd.beat(phase="timed region")
     if sharded:
         barrier("before the timed region")
+    # the host polls the warmup's completion before the opening synchronize
+    # (it stays awake instead of sleeping in the driver's blocking wait: the
+    # first timed step's enqueue 12 -> 7 us, tools/host_steps.py prespin)
+    ewu = torch.cuda.Event()
+    ewu.record()
+    while not ewu.query():
+        pass
     torch.cuda.synchronize()
     # the library launches on torch's current stream: these events bracket
     # every launch (instrumentation, recorded before the host clock starts)
