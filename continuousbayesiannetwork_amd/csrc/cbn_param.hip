@@ -91,9 +91,7 @@ struct alignas(16) PHead {
     float scale;
     float inv_scale;
     float norm;
-    float lw[5];   // linear models (n_layers 1): [w0..w3, bias] zero-padded -- the weights arrive with the
-                   // header, one factor ahead, instead of a dependent scalar load at the factor (round 4)
-    int pad;
+    int pad[6];
 };
 static_assert(sizeof(PHead) == 64, "PHead layout");
 constexpr int kHeadFloats = sizeof(PHead) / 4;
@@ -797,7 +795,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 } else {
                     float mu;
                     if (HMAX == 0 || h.n_layers == 1) {
-                        mu = lin4(h.lw, z);
+                        mu = lin4(img + h.wp, z);
                     } else {
                         const float* PW = img + h.wp;
                         switch (h.act) {
@@ -1620,7 +1618,6 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     const long long cst_off = (long long)n_factors * kRecFloats;  // {0, 1}: constant model inputs
     long long off = cst_off + 4 + (long long)n_factors * kHeadFloats;  // then the PHead array
     std::vector<int> lw_off(n_factors, 0);  // linear models with <= kTabIn inputs: [w0..w3, bias] copy
-    std::vector<float> lw_host((size_t)n_factors * 8, 0.f);  // ... and its host copy (PHead::lw)
     int ns = 0, hmax = 0;
     for (int f = 0; f < n_factors; ++f) {
         const cbn_param_factor& h = factors[f];
@@ -1813,7 +1810,6 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             ok = hipMemcpy(w.data(), h.model.weights, sizeof(float) * (n + 1), hipMemcpyDeviceToHost) == hipSuccess;
             for (int i = 0; i < n; ++i) lw[i] = w[i];
             lw[kTabIn] = w[n];
-            for (int i = 0; i <= kTabIn; ++i) lw_host[(size_t)f * 8 + i] = lw[i];
             ok = ok && hipMemcpy(pp->d_image + lw_off[f], lw.data(), sizeof(float) * 8, hipMemcpyHostToDevice) == hipSuccess;
         }
     }
@@ -1833,7 +1829,6 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             hh.scale = r.scale;
             hh.inv_scale = r.inv_scale;
             hh.norm = r.norm;
-            for (int i = 0; i <= kTabIn; ++i) hh.lw[i] = lw_host[(size_t)f * 8 + i];
         }
         ok = hipMemcpy(pp->d_image + cst_off + 4, heads.data(), sizeof(PHead) * n_factors, hipMemcpyHostToDevice) ==
              hipSuccess;
