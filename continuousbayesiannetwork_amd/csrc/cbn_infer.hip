@@ -568,23 +568,6 @@ struct alignas(16) FastRec {
 constexpr int kDenseBit = 1 << 30;
 constexpr int kRecFloats = sizeof(FastRec) / 4;
 
-// k_query_cols' compact per-factor record (8 ints): {table_off, n_obs,
-// slot0 | card0 << 16, slot1 | card1 << 16} {slot2 | card2 << 16, slot3 |
-// card3 << 16, 0, 0} -- one broadcast LDS read per factor of <= 2 observed
-// parents instead of the FastRec's field-by-field reads (slots < 2^16, cards
-// <= 32767: the kernel's eligibility)
-inline std::vector<int> colrecs(const std::vector<FastRec>& recs) {
-    std::vector<int> c(recs.size() * 8, 0);
-    for (size_t f = 0; f < recs.size(); ++f) {
-        int* x = &c[f * 8];
-        x[0] = recs[f].table_off;
-        x[1] = recs[f].n_obs;
-        for (int p = 0; p < recs[f].n_obs && p < kFastObs; ++p)
-            x[2 + p] = (recs[f].slot[p] & 0xffff) | ((recs[f].card[p] & (kDenseBit - 1)) << 16);
-    }
-    return c;
-}
-
 // Fast path: the L = N / (4 VPL) lanes of one query (a power of two dividing
 // 64, so a query never straddles waves) split its factors: lane l loads the
 // evidence of factors l, l+L, ... (all loads issued before any is used),
@@ -1074,7 +1057,7 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     float* simg = reinterpret_cast<float*>(smem4);
     if (USE_LDS) lds_tab = 0;
     // LDS: [tables (USE_LDS: the whole image) | small tables][records][slot records][slot ptrs][idx][wave max]
-    const int recs_floats = nf * kRecFloats + ns * 4 + nf * 8;  // FastRec[nf], QSlot[ns], colrecs[nf]: contiguous
+    const int recs_floats = nf * kRecFloats + ns * 4;  // FastRec[nf] then QSlot[ns], contiguous in the image
     const int lrec = USE_LDS ? rec_off : lds_tab;      // float offset of the records in LDS
     const float** sptr = reinterpret_cast<const float**>(simg + (USE_LDS ? image_floats : lds_tab + recs_floats));
     const int tid = threadIdx.x;
@@ -1096,8 +1079,8 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     __syncthreads();
     CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
+    const FastRec* rec = reinterpret_cast<const FastRec*>(simg + lrec);
     const QSlot* srec = reinterpret_cast<const QSlot*>(simg + lrec + nf * kRecFloats);
-    const int4* crec = reinterpret_cast<const int4*>(simg + lrec + nf * kRecFloats + ns * 4);  // colrecs[nf]
 
     float maxv = 1.f;
     if (MODE == kModeWrite) {
@@ -1162,20 +1145,16 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                 const int f = f0 + k;
                 int o = -1;
                 if (f < nf) {
-                    // compact record: one broadcast ds_read_b128 (a second one
-                    // only for factors with > 2 observed parents)
-                    const int4 ca = crec[2 * f];
-                    const int4 cb = ca.y > 2 ? crec[2 * f + 1] : make_int4(0, 0, 0, 0);
-                    const int sc[kFastObs] = {ca.z, ca.w, cb.x, cb.y};
-                    o = ca.x;
+                    const FastRec& r = rec[f];
+                    o = r.table_off;
                     int row = 0;
                     bool ok = true;
 #pragma unroll
                     for (int p = 0; p < kFastObs; ++p) {
-                        if (p < ca.y) {
-                            const int i = sidx[(sc[p] & 0xffff) * QB + ql];
+                        if (p < r.n_obs) {
+                            const int i = sidx[r.slot[p] * QB + ql];
                             ok &= i >= 0;
-                            row = row * (sc[p] >> 16) + (i < 0 ? 0 : i);
+                            row = row * (r.card[p] & (kDenseBit - 1)) + (i < 0 ? 0 : i);
                         }
                     }
                     o = ok ? o + row * RS : -1;
@@ -2320,7 +2299,6 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     const long long rec_off = off;  // FastRec array (fast path), copied to LDS with the tables
     off += (long long)n_factors * kRecFloats;
     off += (long long)ns * 4;  // QSlot array right after it (k_query_cols: one LDS-DMA for both)
-    off += (long long)n_factors * 8;  // then the compact records (colrecs, k_query_cols)
     if (off >= (1LL << 30)) return set_err(CBN_E_LIMIT, "plan image too large");
 
     cbn_plan* P = new cbn_plan();
@@ -2481,8 +2459,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 const size_t QBc = (size_t)kQueryThreads / Lf;
                 const size_t cols_bytes =
                     ((P->use_lds ? img_bytes
-                                 : (size_t)P->lds_tab_floats * 4 +
-                                       ((size_t)n_factors * (kRecFloats + 8) + (size_t)ns * 4) * 4) +
+                                 : (size_t)P->lds_tab_floats * 4 + ((size_t)n_factors * kRecFloats + (size_t)ns * 4) * 4) +
                      (size_t)((ns + 1) & ~1) * sizeof(void*) + (((size_t)ns * QBc + 1) & ~size_t(1)) * 2 +
                      (kQueryThreads / kWave) * 4 + 64 + 15) & ~size_t(15);
                 if (ok_c && cols_bytes <= (size_t)kLdsBudget) {
@@ -2495,9 +2472,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
                     hipSuccess ||
                 (ns > 0 && hipMemcpy(P->d_image + rec_off + (long long)n_factors * kRecFloats, qs.data(),
-                                     sizeof(QSlot) * ns, hipMemcpyHostToDevice) != hipSuccess) ||
-                hipMemcpy(P->d_image + rec_off + (long long)n_factors * kRecFloats + (long long)ns * 4,
-                          colrecs(recs).data(), sizeof(int) * 8 * n_factors, hipMemcpyHostToDevice) != hipSuccess) {
+                                     sizeof(QSlot) * ns, hipMemcpyHostToDevice) != hipSuccess)) {
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
             }
