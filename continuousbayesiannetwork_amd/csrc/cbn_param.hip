@@ -758,18 +758,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
     const int tasks = QW * L;
     const int parts = sp.parts;
     const int gpb = wpb / parts;  // query groups per block
-    // wave -> (query group, factor part).  Swizzled (round 4) so the waves a
-    // SIMD holds run DIFFERENT parts: with part = wid % parts every SIMD got
-    // the same part from every block (waves are spread over the SIMDs by
-    // wid % 4), i.e. 8 waves issuing the same instruction stream in
-    // lockstep and stalling on the same scalar loads together.  The product
-    // order within a (group, part) -- and so every bit -- is unchanged.
-    const int grp = wid / parts;
-#ifndef CBN_NO_PART_SWIZZLE
-    const int part = (wid + wid / 4 + (int)blockIdx.x + (int)blockIdx.x / 256) % parts;
-#else
-    const int part = wid % parts;
-#endif
+    const int part = wid % parts, grp = wid / parts;
     const int f0 = sp.f[part], f1 = sp.f[part + 1];
     float* comb = reinterpret_cast<float*>(smem_q) + sp.comb_off;  // [wpb][NC][64]
     float lmax = 0.f;
@@ -866,17 +855,16 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
         }
         if (parts > 1) {
-            // comb slot of (group, part): grp * parts + part
-            float* gslot = comb + (grp * parts * NC) * kWave + lane;
+            float* mine = comb + (wid * NC) * kWave + lane;
             if (part != 0 && active) {
 #pragma unroll
-                for (int j = 0; j < NC; ++j) gslot[(part * NC + j) * kWave] = acc[j];
+                for (int j = 0; j < NC; ++j) mine[j * kWave] = acc[j];
             }
             __syncthreads();
             if (part == 0 && active) {
                 for (int p = 1; p < parts; ++p) {
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * gslot[(p * NC + j) * kWave];
+                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
                 }
             }
             __syncthreads();
