@@ -96,8 +96,6 @@ def parse(argv=None):
     ap.add_argument("--batches", type=int, default=64,
                     help="distinct evidence batches cycled through (64 x 5 MB > the 256 MB Infinity Cache, so "
                          "evidence is read from HBM, not from a cache warmed by the previous step)")
-    ap.add_argument("--no-prespin", action="store_true",
-                    help="sleep in the opening synchronize instead of polling the warmup's completion first (A/B)")
     ap.add_argument("--no-touch", action="store_true",
                     help="do not read every evidence batch once on the device during setup (first-touch A/B)")
     ap.add_argument("--two-pass", action="store_true", help="force the two-launch (max, write) path")
@@ -423,14 +421,6 @@ def main():
         wd.beat(phase="timed region")
     if sharded:
         barrier("before the timed region")
-    # the host polls the warmup's completion before the opening synchronize
-    # (it stays awake instead of sleeping in the driver's blocking wait: the
-    # first timed step's enqueue 12 -> 7 us, tools/host_steps.py prespin)
-    if not a.no_prespin:
-        ewu = torch.cuda.Event()
-        ewu.record()
-        while not ewu.query():
-            pass
     torch.cuda.synchronize()
     # the library launches on torch's current stream: these events bracket
     # every launch (instrumentation, recorded before the host clock starts)
