@@ -109,7 +109,8 @@ wd.arm(phase="timed region")
 x = torch.zeros(1)
 for i in range(1, 1000):
     if rank == 1 and i > 3:
-        time.sleep(600)  # rank 1 stops issuing steps
+        wd.disarm()  # rank 1 stops issuing steps (busy elsewhere, not stuck: only rank 0 must report)
+        time.sleep(600)
     wd.beat(step=i, op="all_reduce(max) of the block max words")
     dist.all_reduce(x, op=dist.ReduceOp.MAX)
 print("unreachable", flush=True)
