@@ -195,7 +195,7 @@ def _ring_worker(rank, world, port, G, gather, out_dir):
     dist.destroy_process_group()
 
 
-def _ring_case(tmp_path, G, gather):
+def _ring_case(tmp_path, G, gather, world=2):
     import json
     import sys
 
@@ -204,19 +204,19 @@ def _ring_case(tmp_path, G, gather):
     from helpers import chain_data, sample_evidence
     from oracle.ref_infer import OracleBN
 
-    mp.spawn(_ring_worker, args=(2, _free_port(), G, gather, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_ring_worker, args=(world, _free_port(), G, gather, str(tmp_path)), nprocs=world, join=True)
     data, cols, edges = chain_data(6, 4, 3000, 7, stay=0.6)
     ora = OracleBN(edges, cols, data)
     for k, Q in enumerate(SIZES):
         ref, _ = ora.infer("X5", sample_evidence(data, cols, ["X4", "X2"], Q, 40 + k), 4)
-        for r in range(2):
+        for r in range(world):
             got = np.load(tmp_path / f"r{r}_s{k}.npy")
-            lo, hi = shard_bounds(Q, 2, r)
+            lo, hi = shard_bounds(Q, world, r)
             np.testing.assert_array_equal(got, ref if gather else ref[lo:hi])
-    logs = [json.load(open(tmp_path / f"log{r}.json")) for r in range(2)]
-    # both ranks issue the same collectives in the same order
+    logs = [json.load(open(tmp_path / f"log{r}.json")) for r in range(world)]
+    # every rank issues the same collectives in the same order
     coll = [[e for e in lg if e[0] in ("exchange", "gather")] for lg in logs]
-    assert coll[0] == coll[1]
+    assert all(c == coll[0] for c in coll[1:])
     # groups: full groups of G, a partial flush at the mid-stream wait() and at the end
     ex = [e[2] for e in coll[0] if e[0] == "exchange"]
     assert sum(ex) == len(SIZES) and max(ex) <= G
@@ -234,6 +234,14 @@ def test_step_ring_two_ranks_rank_local(tmp_path):
 def test_step_ring_two_ranks_gather(tmp_path):
     """Same, with the reassembly: every rank ends with the full [Q, N] tensor."""
     _ring_case(tmp_path, 2, gather=True)
+
+
+def test_step_ring_four_ranks_gather(tmp_path):
+    """Four ranks (the driver's N = 4 scaling point): batches of 1, 2 and 7
+    rows leave three, two and one shards empty or ragged; every rank still
+    ends with the unsharded oracle's full tensor and all four issue the same
+    collectives."""
+    _ring_case(tmp_path, 3, gather=True, world=4)
 
 
 # ---------------------------------------------------------------------------
