@@ -1045,13 +1045,31 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // issue many clamped duplicate loads (configs[4]: 99 slots over 8 lanes = 13)
 constexpr int kColKB = 6;  // factors' rows in flight per gather batch
 
+// Per-factor record of the product loop (round 4, second form).  Lane f of
+// every wave loads factor f's record once (nf <= 64); the loop takes each
+// field with v_readlane into an SGPR -- no memory wait -- so it branches on
+// SGPRs only, issues a whole batch's index reads, then its row reads, each
+// with one wait, and gathers rows with ds_read_b128 (LDS tables) or
+// global_load_dwordx4 (the image), never flat loads.  The first form read
+// FastRec fields from LDS: the compiler serialised field read ->
+// readfirstlane -> branch (3-5 dependent LDS round trips per factor) and
+// gathered through flat loads.  (s_load of this record per factor measured
+// the same.)  configs[2]: X35 27.6 -> 26.7 us, X36 21.6 -> 19.9 us.
+struct alignas(16) ColRec {
+    int base;            // float offset of the table (LDS copy when `lds`, else the image)
+    int n_obs;           // observed parents (<= kFastObs)
+    int par[kFastObs];   // (evidence slot << 24) | row weight in floats (= stride x RS, < 2^24)
+    int lds;             // 1: table is in LDS
+    int pad;
+};
+constexpr int kColRecInts = sizeof(ColRec) / 4;
+
 template <int VPL, bool USE_LDS, int MODE, int CH>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int image_floats,
              FPtrsT<kFastPtrsSmall> sp, long long Q, long long per, int N, int RS, int L,
              unsigned* __restrict__ sync, unsigned epoch, const unsigned* __restrict__ max_in, int n_max,
-             unsigned* __restrict__ max_out, float* __restrict__ out, int lds_tab, unsigned long long lmask0,
-             unsigned long long lmask1) {
+             unsigned* __restrict__ max_out, float* __restrict__ out, int lds_tab, const int* __restrict__ crec) {
     CBN_STAMP_INIT;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
@@ -1065,6 +1083,10 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     const int QB = nthr / L;  // queries per block round
     short* sidx = reinterpret_cast<short*>(sptr + ((ns + 1) & ~1));  // [ns][QB]
     float* wmax = reinterpret_cast<float*>(sidx + (((size_t)ns * QB + 1) & ~size_t(1)));
+    // a zero row (N <= 16 floats, 16-B aligned) after the wave maxima: the row
+    // of an off-domain evidence value (the reference's factor value 0)
+    const int zoff = (int)(((reinterpret_cast<uintptr_t>(wmax + nthr / kWave) - reinterpret_cast<uintptr_t>(simg)) + 15) &
+                           ~uintptr_t(15)) / 4;
     const int lane = tid & (kWave - 1);
     const int wid = tid / kWave;
     const long long q0 = (long long)blockIdx.x * per;
@@ -1075,11 +1097,11 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         lds_dma_copy(gimage + rec_off, smem4 + lds_tab / 4, recs_floats / 4);
     }
     if (tid < ns) sptr[tid] = sp.p[tid];
+    if (tid < N) simg[zoff + tid] = 0.f;
     CBN_STAMP(1);
     __syncthreads();
     CBN_STAMP(2);
     const float* img = USE_LDS ? simg : gimage;
-    const FastRec* rec = reinterpret_cast<const FastRec*>(simg + lrec);
     const QSlot* srec = reinterpret_cast<const QSlot*>(simg + lrec + nf * kRecFloats);
 
     float maxv = 1.f;
@@ -1089,6 +1111,13 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         m = wave_max_u(m);
         maxv = __uint_as_float(m);
         if (max_out && blockIdx.x == 0 && tid == 0) *max_out = m;
+    }
+    // the product loop's records, lane f <- factor f (nf <= 64, host-checked)
+    int4 cra, crb;
+    {
+        const int4* cr = reinterpret_cast<const int4*>(crec) + (size_t)(lane < nf ? lane : (nf > 0 ? nf - 1 : 0)) * (kColRecInts / 4);
+        cra = cr[0];
+        crb = cr[1];
     }
     float lmax = 0.f;
     const int ql = tid / L;        // this lane's query within the block round
@@ -1139,38 +1168,59 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         for (int f0 = 0; f0 < nf; f0 += kColKB) {
+            // the batch's records: lane f holds factor f's, v_readlane -> SGPRs
+            // (a partial batch re-reads the last record; its product is skipped)
+            int base[kColKB], nob[kColKB], inl[kColKB], iv[kColKB][kFastObs], wt[kColKB][kFastObs];
+#pragma unroll
+            for (int k = 0; k < kColKB; ++k) {
+                const int f = f0 + k < nf ? f0 + k : nf - 1;
+                base[k] = __builtin_amdgcn_readlane(cra.x, f);
+                nob[k] = __builtin_amdgcn_readlane(cra.y, f);
+                inl[k] = USE_LDS ? 1 : __builtin_amdgcn_readlane(crb.z, f);
+                // every observed parent's domain index of the batch (one LDS round trip)
+#pragma unroll
+                for (int p = 0; p < kFastObs; ++p) {
+                    iv[k][p] = 0;
+                    wt[k][p] = 0;
+                    if (p < nob[k]) {
+                        const int par = __builtin_amdgcn_readlane(p == 0 ? cra.z : p == 1 ? cra.w : p == 2 ? crb.x : crb.y, f);
+                        iv[k][p] = sidx[(par >> 24) * QB + ql];
+                        wt[k][p] = par & 0xFFFFFF;
+                    }
+                }
+            }
+            // row offset = base + sum(index x weight) (the mixed-radix row of
+            // k_query_fast times RS); any index < 0 (off-domain) -> the zero row
+            // (absent parents add 0 x 0 branch-free: skipping them behind a
+            // second round of uniform branches measured 27 -> 43 us on X35)
             int oo[kColKB];
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
-                const int f = f0 + k;
-                int o = -1;
-                if (f < nf) {
-                    const FastRec& r = rec[f];
-                    o = r.table_off;
-                    int row = 0;
-                    bool ok = true;
+                int o = base[k], neg = 0;
 #pragma unroll
-                    for (int p = 0; p < kFastObs; ++p) {
-                        if (p < r.n_obs) {
-                            const int i = sidx[r.slot[p] * QB + ql];
-                            ok &= i >= 0;
-                            row = row * (r.card[p] & (kDenseBit - 1)) + (i < 0 ? 0 : i);
-                        }
-                    }
-                    o = ok ? o + row * RS : -1;
+                for (int p = 0; p < kFastObs; ++p) {
+                    neg |= iv[k][p];
+                    o += (int)__umul24((unsigned)iv[k][p], (unsigned)wt[k][p]);
                 }
-                oo[k] = o;
+                oo[k] = neg < 0 ? -1 : o;
             }
             float4 t[kColKB][VPL];
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
-                const int o = oo[k];
-                const int fk = f0 + k;
-                const bool in_lds = USE_LDS || (fk < nf && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0));
-                const float* base = in_lds ? simg : img;
-                const float4* row = reinterpret_cast<const float4*>(base + (o < 0 ? 0 : o)) + l * VPL;
+                if (inl[k]) {  // wave-uniform: LDS table (ds_read_b128)
+                    const float4* row = reinterpret_cast<const float4*>(simg + (oo[k] < 0 ? zoff : oo[k])) + l * VPL;
 #pragma unroll
-                for (int v = 0; v < VPL; ++v) t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (int v = 0; v < VPL; ++v) t[k][v] = row[v];
+                } else {  // global table (global_load_dwordx4)
+                    typedef float f4v_t __attribute__((ext_vector_type(4)));
+                    typedef const __attribute__((address_space(1))) f4v_t gf4v_t;
+                    gf4v_t* row = (gf4v_t*)(gimage + (oo[k] < 0 ? 0 : oo[k])) + l * VPL;
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        const f4v_t x = row[v];
+                        t[k][v] = oo[k] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(x.x, x.y, x.z, x.w);
+                    }
+                }
             }
 #pragma unroll
             for (int k = 0; k < kColKB; ++k) {
@@ -1867,7 +1917,7 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
         hipLaunchKernelGGL(k, dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
                            p->rec_off, p->nf, p->ns, p->d_image, p->image_floats, slot_ptrs(p, ev), Q,
                            (Q + blocks - 1) / blocks, p->N, p->RS, L, p->d_sync, epoch, max_in, n_max, max_out, out,
-                           p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
+                           p->lds_tab_floats, p->d_crec);
         return;
     }
     if (p->nf * kFastObs <= kFastPtrsSmall)
@@ -2450,7 +2500,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             // per-slot index buffer fits LDS.  With more lanes per query every
             // lane re-forms every factor's offset: the configs[4] grid (L = 8)
             // ran 459 -> 534 us at 262 144 queries (profiles/r04_cols_ab.json)
-            if (!P->staged && !P->paired && Lf <= 2 && ns <= kFastPtrsSmall && !getenv("CBN_NO_COLS")) {
+            if (!P->staged && !P->paired && Lf <= 2 && ns <= kFastPtrsSmall && n_factors <= kWave &&
+                !getenv("CBN_NO_COLS")) {
                 bool ok_c = true;
                 for (int sl = 0; sl < ns; ++sl) ok_c = ok_c && slot_card[sl] <= 32767;
                 for (int f = 0; f < n_factors && ok_c; ++f)
@@ -2461,8 +2512,30 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                     ((P->use_lds ? img_bytes
                                  : (size_t)P->lds_tab_floats * 4 + ((size_t)n_factors * kRecFloats + (size_t)ns * 4) * 4) +
                      (size_t)((ns + 1) & ~1) * sizeof(void*) + (((size_t)ns * QBc + 1) & ~size_t(1)) * 2 +
-                     (kQueryThreads / kWave) * 4 + 64 + 15) & ~size_t(15);
+                     (kQueryThreads / kWave) * 4 + 64 + 16 + (size_t)N * 4 + 15) & ~size_t(15);  // (+ zero row)
+                // the product loop's scalar records: (slot << 24) | row weight, weights < 2^24
+                std::vector<ColRec> cr(n_factors);
+                for (int f = 0; f < n_factors && ok_c; ++f) {
+                    ColRec& c = cr[f];
+                    memset(&c, 0, sizeof(c));
+                    c.base = recs[f].table_off;
+                    c.n_obs = recs[f].n_obs;
+                    c.lds = P->use_lds || ((lds_mask[f >> 6] >> (f & 63)) & 1ull) ? 1 : 0;
+                    long long w = RS;
+                    for (int q = recs[f].n_obs - 1; q >= 0; --q) {
+                        ok_c = ok_c && w < (1LL << 24) && recs[f].slot[q] < 256;
+                        c.par[q] = (recs[f].slot[q] << 24) | (int)(w & 0xFFFFFF);
+                        w *= recs[f].card[q] & (kDenseBit - 1);
+                    }
+                }
                 if (ok_c && cols_bytes <= (size_t)kLdsBudget) {
+                    ok_c = hipMalloc(&P->d_crec, sizeof(ColRec) * n_factors) == hipSuccess &&
+                           hipMemcpy(P->d_crec, cr.data(), sizeof(ColRec) * n_factors, hipMemcpyHostToDevice) ==
+                               hipSuccess;
+                    if (!ok_c) {
+                        cbn_plan_destroy(P);
+                        return set_err(CBN_E_HIP, "cbn_plan_create: column records upload failed");
+                    }
                     P->cols = true;
                     P->fast_lds_bytes = cols_bytes;
                 }
@@ -2522,6 +2595,7 @@ int cbn_plan_destroy(cbn_plan* plan) {
         for (int k = 0; k < 3; ++k)
             if (plan->ev[i][k]) (void)hipEventDestroy(plan->ev[i][k]);
     if (plan->d_fac) (void)hipFree(plan->d_fac);
+    if (plan->d_crec) (void)hipFree(plan->d_crec);
     if (plan->d_slots) (void)hipFree(plan->d_slots);
     if (plan->d_build) (void)hipFree(plan->d_build);
     if (plan->d_image) (void)hipFree(plan->d_image);

@@ -67,6 +67,7 @@ struct cbn_plan {
     int L = 1;
     int CH = 1;  // queries per block chunk (LDS-sized)
     cbn::DevFactor* d_fac = nullptr;
+    int* d_crec = nullptr;       // k_query_cols: per-factor scalar records (ColRec)
     cbn::QSlot* d_slots = nullptr;
     cbn::BuildItem* d_build = nullptr;
     int n_build = 0;

@@ -464,6 +464,42 @@ def test_alarm_like_config2_matches_oracle(target, N, missing, gpu):
     np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
 
 
+def test_config2_cols_off_domain_rows_through_lds_and_global_tables(gpu):
+    """configs[2]'s kernel (k_query_cols, CBN_PLAN_COLS) with off-domain
+    evidence on a parent of a 4 096-row table (gathered from the image in
+    global memory) and on a parent of an 8-row table (in LDS): those rows are
+    all zero (BruteForce gives 0 outside the fitted domain, brute_force.py:
+    172-244), every other row matches the oracle at rtol 1e-5."""
+    from continuousbayesiannetwork_amd import _native
+
+    data, cols, edges = alarm_like_data(50000, 5)
+    par = {c: [] for c in cols}
+    for a, b in edges:
+        par[b].append(a)
+    anc, todo = set(), ["X35"]
+    while todo:
+        for p in par[todo.pop()]:
+            if p not in anc:
+                anc.add(p)
+                todo.append(p)
+    fam = sorted(anc) + ["X35"]
+    p4 = par[next(n for n in fam if len(par[n]) == 4)][0]
+    p1 = next(par[n][0] for n in fam if len(par[n]) == 1 and par[n][0] != p4)
+    names = [c for c in cols if c != "X35"]
+    ev = sample_evidence(data, cols, names, 512, 21)
+    ev[p4][:64] = 99.0
+    ev[p1][64:128] = -3.0
+    ev[p1][128:130] = 2.5  # between two domain values
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    pdf, _ = bn.infer("X35", _t(ev, gpu), N_max=8)
+    fp = bn.engine._fast[("X35", tuple(ev.keys()), 8)]
+    assert _native.load().cbn_plan_flags(fp.plan.handle) & _native.CBN_PLAN_COLS
+    p = pdf.cpu().numpy()
+    assert (p[:130] == 0).all() and p.max() == 1.0
+    ref, _ = OracleBN(edges, cols, data).infer("X35", ev, 8)
+    np.testing.assert_allclose(p, ref, rtol=RTOL, atol=ATOL)
+
+
 def test_alarm_like_config2_full_batch_properties(gpu):
     """262 144 queries (configs[2] size): max exactly 1; rows of duplicated
     evidence identical; a sample of rows plus the batch argmax row matches the
