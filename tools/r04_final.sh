@@ -3,9 +3,9 @@
 # (x3), the default bench, and the configs[2] / [3] / [4] benches
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
-mkdir -p gpurun_out/r04z
+mkdir -p gpurun_out/${OUT:-r04z}
 export TMPDIR=/tmp
-O=gpurun_out/r04z
+O=gpurun_out/${OUT:-r04z}
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -2 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
