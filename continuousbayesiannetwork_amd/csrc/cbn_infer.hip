@@ -1043,7 +1043,15 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // CH: slot loads in flight per lane (all of a lane's slots in one round trip
 // when ceil(ns / L) <= CH): 16 or 40, picked per plan, so a lane does not
 // issue many clamped duplicate loads (configs[4]: 99 slots over 8 lanes = 13)
-constexpr int kColKB = 6;  // factors' rows in flight per gather batch
+#ifndef CBN_COL_KB
+#define CBN_COL_KB 2
+#endif
+// factors per gather batch.  Measured on one box (profiles/r04_colrec_ab.json),
+// X35 / X36 / N = 16 chain at 262 144 queries, us: KB 6: 26.8 / 19.9 / 36.4;
+// 4: 25.4 / 20.2 / 31.8; 2: 23.9 / 19.2 / 30.4; 1: 23.4 / 18.9 / 31.4; 8: 28.7.
+// Smaller batches win: more waves are past their waits at any time (4 waves
+// per SIMD), and fewer rows sit in VGPRs.
+constexpr int kColKB = CBN_COL_KB;
 
 // Per-factor record of the product loop (round 4, second form).  Lane f of
 // every wave loads factor f's record once (nf <= 64); the loop takes each
