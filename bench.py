@@ -63,7 +63,17 @@ from continuousbayesiannetwork_amd.distributed import ShardedStepper, Watchdog  
 from helpers import chain_data, make_bn, sample_evidence  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-XGMI_PEAK_GBS = 7 * 153.0  # 7 xGMI links x ~153 GB/s per GPU (incoming), the reassembly's bound at N > 1
+# xGMI: 7 links per GPU at ~153 GB/s each -- the figure of the task brief;
+# the microarchitecture guide gives none, and whether 153 GB/s is per
+# direction or both directions together is not stated.  Both readings are
+# carried: the incoming peak is 7 x 153 if per direction, half
+# of that if bidirectional.
+XGMI_LINKS, XGMI_LINK_GBS = 7, 153.0
+XGMI_PEAK_GBS = XGMI_LINKS * XGMI_LINK_GBS  # incoming, 153 GB/s per link per direction (assumed)
+XGMI_PEAK_BIDIR_GBS = XGMI_PEAK_GBS / 2  # incoming, if 153 GB/s is the bidirectional per-link figure
+LINK_ASSUMPTION = ("assumed: 7 xGMI links x 153 GB/s per GPU (task brief; not in MI355X_MICROARCH.md), taken as "
+                   "per direction (incoming peak 1071 GB/s); '_if_bidirectional' fields take it as both directions "
+                   "together (incoming 535.5 GB/s)")
 
 
 def pmc_traffic(kernel: str):
@@ -256,18 +266,38 @@ def step_modes(a, world: int) -> dict:
 def projection(world: int) -> dict:
     """DESIGN.md (Multi-GPU) bound on the gathered step: every rank receives
     (N-1) x 8.4 MB of rows per step over its 7 xGMI links and writes N x 8.4 MB
-    of marginals -- a projection, not a measurement."""
+    of marginals -- a projection, not a measurement, under either reading of
+    the link figure (LINK_ASSUMPTION)."""
     rows_b = 65536 * 32 * 4
-    t_link = (world - 1) * rows_b / (XGMI_PEAK_GBS * 1e9)
     t_write = world * rows_b / (HBM_PEAK_GBS * 1e9)
     t_one = 10.3e-6
     t_ring = 16.7e-6  # step ring at N=1 (raw launch + batched scale + all-reduce): 15.7 us + ~1 us interference
-    return {"gathered_x_vs_1gpu": round(world * t_one / max(t_ring, t_link, t_write), 2),
+
+    def gathered(peak_gbs):
+        t_link = (world - 1) * rows_b / (peak_gbs * 1e9)
+        return round(world * t_one / max(t_ring, t_link, t_write), 2)
+
+    return {"gathered_x_vs_1gpu": gathered(XGMI_PEAK_GBS),
+            "gathered_x_vs_1gpu_if_bidirectional": gathered(XGMI_PEAK_BIDIR_GBS),
             "rank_local_x_vs_1gpu": round(world * t_one / t_ring, 2) if world > 1 else 1.0,
+            "link_assumption": LINK_ASSUMPTION,
+            "status": "projection, not a measurement: no run with >= 2 GPUs has pinned these figures",
             "basis": "DESIGN.md Multi-GPU: gathered step >= max(16.7 us step-ring GPU time, (N-1) x 8.4 MB over "
-                     "7 x 153 GB/s, N x 8.4 MB written at 8 TB/s); rank-local = the step ring (the folded ring is "
-                     "one-rank only until a 2-GPU run pins it): 15.7 us per step measured at N=1 + ~1 us of "
+                     "the incoming xGMI peak, N x 8.4 MB written at 8 TB/s); rank-local = the step ring (the folded "
+                     "ring is one-rank only until a 2-GPU run pins it): 15.7 us per step measured at N=1 + ~1 us of "
                      "collective interference, vs the fused single-GPU 10.3 us"}
+
+
+def multi_gpu_fields(gpus: int, world: int, rccl_ranks) -> dict:
+    """The N > 1 self-checks of the JSON line: ``rccl_ranks`` = the ranks of
+    the stepper's own RCCL communicator as ncclCommCount reports them (None
+    when the step uses none), which must equal --gpus; plus the projection."""
+    if rccl_ranks is not None and rccl_ranks != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the stepper's RCCL communicator has {rccl_ranks} ranks")
+    out = {"rccl_ranks": rccl_ranks}
+    if world > 1:
+        out["projection"] = projection(world)
+    return out
 
 
 def reference_over_port():
@@ -516,6 +546,8 @@ def main():
         achieved = bytes_in / t_step / 1e9
         roofline = dict(bound="xgmi", achieved=round(achieved, 1), peak=XGMI_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / XGMI_PEAK_GBS, 4), traffic=None,
+                        peak_if_bidirectional=XGMI_PEAK_BIDIR_GBS,
+                        frac_if_bidirectional=round(achieved / XGMI_PEAK_BIDIR_GBS, 4), peak_source=LINK_ASSUMPTION,
                         kernel="sharded step: raw launch + ncclAllReduce(MAX) + k_scale_batch + ncclAllGather of "
                                "the [Q, N] rows (per step)",
                         avg_us=round(t_step * 1e6, 2), algorithmic_bytes_per_launch=bytes_in, timed_steps=K,
@@ -544,6 +576,7 @@ def main():
         if tsrc:
             roofline["traffic_source"] = tsrc + " (2 x FETCH_SIZE + WRITE_SIZE per dispatch)"
 
+    rccl_ranks = stepper.comm_ranks() if sharded else None  # before close(): the headline step's communicator
     other = None
     if modes["other_kind"] is not None:
         # the same step with the other reassembly choice: each rank keeping its
@@ -593,8 +626,7 @@ def main():
             "tables": "rebuilt every step" if a.rebuild_tables else "built once per plan",
             "evidence_batches": len(batches),
         }
-        if world > 1:
-            line["projection"] = projection(world)
+        line.update(multi_gpu_fields(a.gpus, world, rccl_ranks))
         if cold is not None:
             line["value_rebuild_tables"] = round(cold, 1)
         if other is not None:

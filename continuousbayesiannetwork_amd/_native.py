@@ -139,6 +139,7 @@ _SIGNATURES = {
     "cbn_plan_fused_capacity": (ctypes.c_int64, [ctypes.c_void_p]),
     "cbn_plan_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "cbn_debug_flag_timeout": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbn_diag_enabled": (ctypes.c_int32, []),
     "cbn_plan_check": (ctypes.c_int, [ctypes.c_void_p]),
     "cbn_plan_flags": (ctypes.c_int32, [ctypes.c_void_p]),
     "cbn_scale": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),

@@ -79,14 +79,18 @@ struct DirectPlan {
     double query_combos = 0;    // sum over QUERY factors of their free-parent combos (per query and column)
 };
 
-// Work bounds: a direct factor's free-parent mean loops over its
-// F = N^(free parents) combos serially per (query, column) -- the reference
-// materialises Q x F x N pdf values for the same factor (node.py:335-375).
-// The plan takes F <= 2^32 (query-independent factors: F x N <= 2^40, once
-// per plan); a call is refused when Q x N x (sum of its QUERY factors' F)
-// exceeds 2^40 CPD lookups (tens of seconds of GPU time): split the batch.
+// Work bounds: a direct factor's free-parent mean loops over
+// its F = N^(free parents) combos serially per (query, column) -- the
+// reference materialises Q x F x N pdf values for the same factor
+// (node.py:335-375).  Two bounds keep every launch short:
+// * per thread (plan time): the serial chain of one (query, column) thread --
+//   the sum of the QUERY factors' F in k_query_direct, one factor's F in
+//   k_direct_const -- is at most 2^26 CPD lookups (~1 s of one thread's
+//   latency-bound loop), so even a one-query call cannot run for minutes;
+// * per call: Q x N x (sum of the QUERY factors' F) <= 2^40 CPD lookups, and
+//   per query-independent factor F x N <= 2^40: split the batch.
 constexpr double kDirectCallLookups = 1099511627776.0;  // 2^40
-constexpr long long kDirectMaxCombos = 1LL << 32;
+constexpr long long kDirectThreadLookups = 1LL << 26;
 
 }  // namespace cbn
 
@@ -182,11 +186,23 @@ __global__ void k_cpd_ref_eval(DevCpd c, int n_cols, RefCols rc, const float* __
 // x_f[j] for query-independent factors (SCALAR: mean over the N node
 // samples, replicated; SHARED: mean over the N^k parent sample combos)
 __device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
+    // the combos in the reference's meshgrid order (c = 0 .. F-1, the last
+    // free parent varying fastest): the outer loop forms the other free
+    // parents' key part (one mixed-radix division chain per N combos), the
+    // inner loop walks the last free parent's N samples -- the same terms in
+    // the same order as one flat loop over c, so the same fp64 sum
+    int pl = -1;
+    for (int p = d.n_parents - 1; p >= 0 && pl < 0; --p)
+        if (d.col[p].ev_slot < 0) pl = p;
+    if (pl < 0) return (double)cpd_get(d.cpd, base);  // F = 1
+    const int* __restrict__ li = d.col[pl].sample_idx;
+    const long long ls = d.col[pl].stride;
+    const long long outer = d.free_combos / N;
     double s = 0.0;  // fp64 sum, one rounding of the mean (see entry_partial, cbn_infer.hip)
-    for (long long c = 0; c < d.free_combos; ++c) {
-        long long key = base, cc = c;
+    for (long long o = 0; o < outer; ++o) {
+        long long key = base, cc = o;
         bool ok = true;
-        for (int p = d.n_parents - 1; p >= 0; --p) {
+        for (int p = pl - 1; p >= 0; --p) {
             const DevDCol& col = d.col[p];
             if (col.ev_slot < 0) {
                 const long long qq = cc / N;
@@ -196,7 +212,11 @@ __device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
                 key += (long long)(pi < 0 ? 0 : pi) * col.stride;
             }
         }
-        s += ok ? (double)cpd_get(d.cpd, key) : 0.0;
+        if (!ok) continue;  // N terms of +0.0: s is unchanged (s >= +0)
+        for (int j = 0; j < N; ++j) {
+            const int pi = li[j];
+            s += pi >= 0 ? (double)cpd_get(d.cpd, key + (long long)pi * ls) : 0.0;
+        }
     }
     return s;
 }
@@ -499,16 +519,22 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
                 c.sample_idx = h.parent_sample_idx + (long long)p * N;
                 ++d.n_free;
                 // each (query, column) thread loops over the F free-parent combos
-                // serially (work bounds: kDirectMaxCombos / kDirectCallLookups)
-                if (F > kDirectMaxCombos / N)
-                    return set_err(CBN_E_LIMIT, "factor %d: more than 2^32 free-parent sample combos", f);
+                // serially (work bounds: kDirectThreadLookups / kDirectCallLookups)
+                if (F > kDirectThreadLookups / N)
+                    return set_err(CBN_E_LIMIT,
+                                   "factor %d: more than 2^26 free-parent sample combos (one thread's serial loop)", f);
                 F *= N;
             }
         }
         d.free_combos = F;
         if ((h.kind == CBN_FACTOR_QUERY) != (d.n_obs > 0)) return set_err(CBN_E_ARG, "factor %d: QUERY iff some parent observed", f);
-        if (h.kind == CBN_FACTOR_QUERY) query_combos += (double)F;
-        else if ((double)F * N > kDirectCallLookups)
+        if (h.kind == CBN_FACTOR_QUERY) {
+            query_combos += (double)F;
+            if (query_combos > (double)kDirectThreadLookups)
+                return set_err(CBN_E_LIMIT,
+                               "factors up to %d: %.0f free-parent combos per (query, column) > 2^26 (one thread's "
+                               "serial loop over every query factor)", f, query_combos);
+        } else if ((double)F * N > kDirectCallLookups)
             return set_err(CBN_E_LIMIT, "factor %d: %lld free-parent combos x %d columns > 2^40 CPD lookups", f, F, N);
         if (h.kind != CBN_FACTOR_QUERY) d.cidx = n_const++;
     }

@@ -33,6 +33,8 @@
 #include <type_traits>
 #include <vector>
 
+#include <unistd.h>  // environ
+
 #include "cbn_internal.h"
 
 using namespace cbn;
@@ -40,6 +42,25 @@ using namespace cbn;
 namespace {
 thread_local std::string g_err;
 }  // namespace
+
+// Diagnostic switches (same-box A/B builds under tools/: CBN_NO_STAGED,
+// CBN_FAST_VPL, CBN_PARAM_GENERIC, ...) are honoured only when CBN_DIAG=1 is
+// set when the library is loaded, so a stray variable in a serving process
+// cannot swap kernels; with CBN_DIAG=1 every CBN_* variable of the
+// environment is listed on stderr at load (ADVICE / VERDICT r04).
+namespace {
+const bool g_diag = [] {
+    const char* e = getenv("CBN_DIAG");
+    const bool on = e && e[0] == '1' && e[1] == 0;
+    if (on)
+        for (char** v = environ; v && *v; ++v)
+            if (!strncmp(*v, "CBN_", 4) && strncmp(*v, "CBN_DIAG=", 9))
+                fprintf(stderr, "[libcbn_amd] CBN_DIAG=1: diagnostic override %s\n", *v);
+    return on;
+}();
+}  // namespace
+
+const char* cbn::diag_env(const char* name) { return g_diag ? getenv(name) : nullptr; }
 
 int cbn::set_err(int code, const char* fmt, ...) {
     char buf[512];
@@ -1990,7 +2011,7 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
 // launch waits for one to finish
 int raw_reserve_cu() {
     static int v = [] {
-        const char* e = getenv("CBN_RAW_RESERVE_CU");
+        const char* e = diag_env("CBN_RAW_RESERVE_CU");
         const int x = e ? atoi(e) : 0;
         return x >= 0 && x <= 64 ? x : 0;
     }();
@@ -2100,6 +2121,8 @@ int cbn_debug_set_check_buffer(void* dev_ptr) {
 
 // Test hook: mark the plan's host-mapped status as if a fused launch had timed
 // out (the reporting path of CBN_E_TIMEOUT without starving the GPU).
+int32_t cbn_diag_enabled(void) { return g_diag ? 1 : 0; }
+
 int cbn_debug_flag_timeout(cbn_plan* plan) {
     if (!plan || !plan->h_status) return set_err(CBN_E_ARG, "cbn_debug_flag_timeout: plan has no status word");
     __atomic_store_n(plan->h_status, 1u, __ATOMIC_RELEASE);
@@ -2191,7 +2214,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     // layout's random rows collide ~2x, profiles/r02_lds_pmc.txt).
     long long class_rows[2] = {0, 0};
     int want_vpl = 2;
-    if (const char* e = getenv("CBN_FAST_VPL")) want_vpl = atoi(e);
+    if (const char* e = diag_env("CBN_FAST_VPL")) want_vpl = atoi(e);
     for (int f = 0; f < n_factors; ++f) {
         long long rows = 1;
         for (int p = 0; p < factors[f].n_parents && p < kMaxP; ++p)
@@ -2199,12 +2222,12 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 rows = std::min(rows * factors[f].parent_card[p], 1LL << 40);
         class_rows[f & 1] += rows;
     }
-    bool paired = vec == 4 && N == 32 && !global_tables && want_vpl >= 2 && !getenv("CBN_NO_PAIRED") &&
+    bool paired = vec == 4 && N == 32 && !global_tables && want_vpl >= 2 && !diag_env("CBN_NO_PAIRED") &&
                   std::max(class_rows[0], class_rows[1]) * 64 * 4 <= (long long)kLdsBudget * 3 / 4;
     // leading 1-row factors (roots / unobserved-parent factors) fold into the
     // first multi-row factor (k_merge_prefix); the staged kernel skips them
     int prefix = 0;
-    if (paired && !getenv("CBN_NO_PREFIX")) {
+    if (paired && !diag_env("CBN_NO_PREFIX")) {
         while (prefix < n_factors - 1 && prefix < 8) {
             long long rows = 1;
             for (int p = 0; p < factors[prefix].n_parents && p < kMaxP; ++p)
@@ -2224,7 +2247,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     std::vector<long long> pre_off(n_factors, -1);
     long long lds_tab_end = 0;
     unsigned long long lds_mask[2] = {0, 0};
-    if (global_tables && vec == 4 && n_factors <= 128 && !getenv("CBN_NO_LDS_SPLIT")) {
+    if (global_tables && vec == 4 && n_factors <= 128 && !diag_env("CBN_NO_LDS_SPLIT")) {
         int vp = 0, Lp = 0;
         for (int c : {2, 1}) {  // the fast path's choice (below)
             if (c > want_vpl || (N / 4) % c) continue;
@@ -2466,7 +2489,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
     int vpl = 0, Lf = 0;
     if (fast) {
         int want = 2;  // 8 output values per lane (tuned on MI355X: chain20 d32)
-        if (const char* e = getenv("CBN_FAST_VPL")) want = atoi(e);
+        if (const char* e = diag_env("CBN_FAST_VPL")) want = atoi(e);
         for (int c : {2, 1}) {  // VPL 4 exceeds 128 VGPRs at 1024 threads (spills)
             if (c > want || (N / 4) % c) continue;
             const int Lc = N / (4 * c);
@@ -2491,7 +2514,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             const size_t st_bytes =
                 img_bytes + (size_t)2 * kSR * (4 * (st_S + 1)) * 4 + (kQueryThreads / kWave) * 4 + 64;
             if (P->paired && (n_factors - P->prefix) * kFastObs <= kFastPtrsSmall && st_bytes <= (size_t)kLdsBudget &&
-                !getenv("CBN_NO_STAGED")) {
+                !diag_env("CBN_NO_STAGED")) {
                 P->staged = true;
                 P->staged_lds_bytes = (st_bytes + 15) & ~size_t(15);
                 for (const void* fn : {reinterpret_cast<const void*>(&k_query_staged<kModeMax>),
@@ -2509,7 +2532,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             // lane re-forms every factor's offset: the configs[4] grid (L = 8)
             // ran 459 -> 534 us at 262 144 queries (profiles/r04_cols_ab.json)
             if (!P->staged && !P->paired && Lf <= 2 && ns <= kFastPtrsSmall && n_factors <= kWave &&
-                !getenv("CBN_NO_COLS")) {
+                !diag_env("CBN_NO_COLS")) {
                 bool ok_c = true;
                 for (int sl = 0; sl < ns; ++sl) ok_c = ok_c && slot_card[sl] <= 32767;
                 for (int f = 0; f < n_factors && ok_c; ++f)
@@ -2557,7 +2580,7 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 cbn_plan_destroy(P);
                 return set_err(CBN_E_HIP, "cbn_plan_create: fast records upload failed");
             }
-            if (!getenv("CBN_NO_FUSED")) {
+            if (!diag_env("CBN_NO_FUSED")) {
                 // the grid barrier needs every block resident: check one block per CU fits
                 // (tables in LDS, or -- image beyond LDS -- read from L2/HBM)
                 allow_fast_lds<1, true, kModeFused>(kLdsBudget);
@@ -2912,7 +2935,7 @@ namespace {
 // blocks per CU of the batched scale (CBN_SCALE_BLOCKS_PER_CU, A/B knob)
 int scale_blocks_per_cu() {
     static int v = [] {
-        const char* e = getenv("CBN_SCALE_BLOCKS_PER_CU");
+        const char* e = diag_env("CBN_SCALE_BLOCKS_PER_CU");
         const int x = e ? atoi(e) : 0;
         return x >= 1 && x <= 16 ? x : 1;
     }();

@@ -38,6 +38,9 @@ struct ParamPlan;  // cbn_param.hip
 struct DirectPlan;  // cbn_direct.hip
 
 int set_err(int code, const char* fmt, ...);
+// getenv(name) when the library was loaded with CBN_DIAG=1, else nullptr
+// (diagnostic kernel-selection switches; cbn_infer.hip)
+const char* diag_env(const char* name);
 int num_cu();
 
 // out[i] /= max(words[0, n_words)) in place on `s`; block 0 also stores that

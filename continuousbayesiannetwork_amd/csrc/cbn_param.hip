@@ -1432,7 +1432,7 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     // (<= 64 VGPRs: 8 waves per SIMD); MLPs keep whole rows up to 32 columns
     // (every extra chunk re-evaluates the network)
     int nc = pp->nc;
-    const bool lin16 = pp->lin16 && !getenv("CBN_PARAM_LIN8");
+    const bool lin16 = pp->lin16 && !diag_env("CBN_PARAM_LIN8");
     if (pp->hmax == 0 && specialised(pp->hmax, pp->mode)) nc = lin16 ? 16 : 8;
     const int L = (pp->N + nc - 1) / nc;
     const long long waves = QW * L;
@@ -1440,7 +1440,7 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
         return set_err(CBN_E_LIMIT, "cbn_plan_run: batch too large for one launch");
     // factor split (ParamPlan::parts; CBN_PARAM_PARTS overrides it for A/B)
     int parts = pp->parts;
-    if (const char* e = getenv("CBN_PARAM_PARTS")) {
+    if (const char* e = diag_env("CBN_PARAM_PARTS")) {
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) parts = v;
     }
@@ -1611,7 +1611,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         HostModel hm;
         const int rc = resolve_model(factors[f].model, hm, "factor", f);
         if (rc) return rc;
-        if (!hm.fast || getenv("CBN_PARAM_GENERIC")) return create_param_generic(factors, n_factors, N, plan);
+        if (!hm.fast || diag_env("CBN_PARAM_GENERIC")) return create_param_generic(factors, n_factors, N, plan);
     }
     std::vector<PRec> recs(n_factors);
     std::vector<int> consts;
@@ -1700,7 +1700,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
         pp->mode = pp->mode < 0 || pp->mode == m ? m : 4;
     }
     if (pp->mode < 0) pp->mode = 0;  // no query factor
-    pp->all_m1 = !getenv("CBN_PARAM_NO_M1");
+    pp->all_m1 = !diag_env("CBN_PARAM_NO_M1");
     for (const PRec& r : recs) pp->all_m1 = pp->all_m1 && (r.kind != CBN_FACTOR_QUERY || r.M == 1);
     // factor split: a plan constant (never a function of the batch size), so
     // the product order -- and every row bit -- is the same however the batch
@@ -1735,7 +1735,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     int nc = 32;
     if (N <= 8) nc = 8;
     else if (N <= 16) nc = 16;
-    if (const char* e = getenv("CBN_PARAM_NC")) {
+    if (const char* e = diag_env("CBN_PARAM_NC")) {
         const int v = atoi(e);
         if (v == 8 || v == 16 || v == 32) nc = v;
     }
@@ -1859,7 +1859,7 @@ int cbn_param_eval(const cbn_param_model* model, const float* points, int64_t n_
     if (rc) return rc;
     if (root_bias_only && hm.n_layers != 1) return set_err(CBN_E_ARG, "cbn_param_eval: bias-only needs a linear model");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (!hm.fast || getenv("CBN_PARAM_GENERIC")) {
+    if (!hm.fast || diag_env("CBN_PARAM_GENERIC")) {
         const int T = gen_threads(hm.wmax);
         if (T == 0) return set_err(CBN_E_LIMIT, "cbn_param_eval: layers of %d units exceed the LDS", hm.wmax);
         if (n_rows == 0 || n_points == 0) return CBN_OK;

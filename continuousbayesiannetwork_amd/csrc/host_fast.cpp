@@ -38,6 +38,17 @@ namespace {
 
 using run_fn = int (*)(void*, int64_t, const float* const*, int32_t, unsigned*, float*, int32_t, hipStream_t);
 
+// Diagnostic A/B switches (CBN_COMM_HIGH_PRIO, CBN_FOLD_EAGER) count only when
+// CBN_DIAG=1 is set, as in libcbn_amd.so (cbn_diag_enabled, include/cbn_amd.h).
+bool diag_switch(const char* name) {
+    static const bool diag = [] {
+        const char* e = getenv("CBN_DIAG");
+        return e && e[0] == '1' && e[1] == 0;
+    }();
+    const char* e = diag ? getenv(name) : nullptr;
+    return e && e[0] == '1';
+}
+
 // Returns the output tensor; None when a fast check failed (the caller takes
 // the slow path); an int = the C ABI's (negative) error code (the caller
 // raises with cbn_last_error()).
@@ -70,8 +81,11 @@ bool gather(py::dict& evidence, py::tuple& slots, py::object& first, int64_t dev
         PyObject* v = PyDict_GetItem(evidence.ptr(), PyTuple_GET_ITEM(slots.ptr(), i));
         if (!v || !THPVariable_Check(v)) return false;
         const at::Tensor& t = THPVariable_Unpack(v);
+        // [n, 1] only: the kernels read element q of the column as query q's
+        // value, and any other width raises in the reference (node.py:233-248;
+        // the Python path raises it)
         if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != device_index || t.dim() != 2 ||
-            t.size(0) != n || !t.is_contiguous())
+            t.size(0) != n || t.size(1) != 1 || !t.is_contiguous())
             return false;
         c.p[i] = static_cast<const float*>(t.data_ptr());
     }
@@ -81,6 +95,25 @@ bool gather(py::dict& evidence, py::tuple& slots, py::object& first, int64_t dev
 }
 
 at::Tensor check_out(py::object& out_obj, int64_t n, int64_t n_samples, int64_t dev);
+
+// An empty shard (the first evidence column has no rows) is a valid sharded
+// step when every slot column is a [0, 1] tensor; a malformed one returns
+// false, so the caller's slow path raises the reference's shape error before
+// any collective of the step is issued.
+bool empty_shard(py::dict& evidence, py::tuple& slots, py::object& first) {
+    if (first.is_none()) return false;
+    PyObject* f = PyDict_GetItem(evidence.ptr(), first.ptr());
+    if (!f || !THPVariable_Check(f)) return false;
+    const at::Tensor& t0 = THPVariable_Unpack(f);
+    if (t0.dim() < 1 || t0.size(0) != 0) return false;
+    for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(slots.ptr()); ++i) {
+        PyObject* v = PyDict_GetItem(evidence.ptr(), PyTuple_GET_ITEM(slots.ptr(), i));
+        if (!v || !THPVariable_Check(v)) return false;
+        const at::Tensor& t = THPVariable_Unpack(v);
+        if (t.dim() != 2 || t.size(0) != 0 || t.size(1) != 1) return false;
+    }
+    return true;
+}
 
 py::object run(uintptr_t fn, uintptr_t plan, py::dict evidence, py::tuple slots, py::object first,
                int64_t device_index, int64_t n_samples, bool target_observed, uintptr_t max_ptr, int32_t flags,
@@ -121,10 +154,7 @@ constexpr unsigned kEvFlags = hipEventDisableTiming | hipEventReleaseToDevice;
 // stream ran at ~52 us per step instead of ~12.5 for as long as the stepper
 // lived.  CBN_COMM_HIGH_PRIO=1 restores the high-priority stream (A/B).
 c10::hip::HIPStream comm_stream(c10::DeviceIndex dev) {
-    static const bool high = [] {
-        const char* e = getenv("CBN_COMM_HIGH_PRIO");
-        return e && e[0] == '1';
-    }();
+    static const bool high = diag_switch("CBN_COMM_HIGH_PRIO");
     return c10::hip::getStreamFromPool(high, dev);
 }
 
@@ -143,6 +173,7 @@ struct Rccl {
     ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
 } g_rccl;
 
@@ -165,6 +196,7 @@ void rccl_load(const std::string& path) {
     g_rccl.broadcast = reinterpret_cast<decltype(g_rccl.broadcast)>(sym("ncclBroadcast"));
     g_rccl.group_start = reinterpret_cast<decltype(g_rccl.group_start)>(sym("ncclGroupStart"));
     g_rccl.group_end = reinterpret_cast<decltype(g_rccl.group_end)>(sym("ncclGroupEnd"));
+    g_rccl.comm_count = reinterpret_cast<decltype(g_rccl.comm_count)>(sym("ncclCommCount"));
 }
 
 #define CBN_NCCL_OK(x)                                                                                   \
@@ -193,6 +225,15 @@ uintptr_t nccl_comm_init(std::string rccl_path, py::bytes id_bytes, int world, i
         CBN_NCCL_OK(g_rccl.comm_init_rank(&comm, world, id, rank));
     }
     return reinterpret_cast<uintptr_t>(comm);
+}
+
+// ranks of one of our communicators as RCCL itself reports them (bench.py's
+// rccl_ranks: the N > 1 line checks it against --gpus)
+int nccl_comm_count(uintptr_t comm) {
+    if (!comm || !g_rccl.comm_count) throw std::invalid_argument("nccl_comm_count: no communicator");
+    int n = 0;
+    CBN_NCCL_OK(g_rccl.comm_count(reinterpret_cast<ncclComm_t>(comm), &n));
+    return n;
 }
 
 void nccl_comm_destroy(uintptr_t comm) {
@@ -428,9 +469,12 @@ class Runner {
         const Py_ssize_t nk = PyTuple_GET_SIZE(keys.ptr());
         for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(slots.ptr()); ++i) {
             Py_ssize_t pos = -1;
-            for (Py_ssize_t j = 0; j < nk && pos < 0; ++j)
-                if (PyObject_RichCompareBool(PyTuple_GET_ITEM(keys.ptr(), j), PyTuple_GET_ITEM(slots.ptr(), i), Py_EQ) == 1)
-                    pos = j;
+            for (Py_ssize_t j = 0; j < nk && pos < 0; ++j) {
+                const int eq =
+                    PyObject_RichCompareBool(PyTuple_GET_ITEM(keys.ptr(), j), PyTuple_GET_ITEM(slots.ptr(), i), Py_EQ);
+                if (eq < 0) throw py::error_already_set();
+                if (eq == 1) pos = j;
+            }
             if (pos < 0) throw std::invalid_argument("Runner: slot key not among the evidence keys");
             slot_pos_.push_back(pos);
         }
@@ -447,7 +491,13 @@ class Runner {
         PyObject *k, *v;
         while (PyDict_Next(d, &it, &k, &v)) {
             PyObject* want = PyTuple_GET_ITEM(keys_.ptr(), j);
-            if (k != want && PyObject_RichCompareBool(k, want, Py_EQ) != 1) return py::none();
+            if (k != want) {
+                const int eq = PyObject_RichCompareBool(k, want, Py_EQ);
+                if (eq != 1) {
+                    if (eq < 0) PyErr_Clear();  // a key whose __eq__ raised: no match, the general path decides
+                    return py::none();
+                }
+            }
             vals_[j++] = v;
         }
         int64_t n = 1;
@@ -464,7 +514,7 @@ class Runner {
             if (!THPVariable_Check(x)) return py::none();
             const at::Tensor& t = THPVariable_Unpack(x);
             if (t.scalar_type() != at::kFloat || !t.is_cuda() || t.get_device() != dev_ || t.dim() != 2 ||
-                t.size(0) != n || !t.is_contiguous())
+                t.size(0) != n || t.size(1) != 1 || !t.is_contiguous())
                 return py::none();
             ptrs_[i] = static_cast<const float*>(t.data_ptr());
         }
@@ -591,15 +641,9 @@ class Stepper {
   private:
     // like gather(), but an empty shard is a valid step (n = 0)
     bool gather_cols(py::dict& evidence, Cols& c, int64_t& n) {
-        if (!first_.is_none()) {
-            PyObject* f = PyDict_GetItem(evidence.ptr(), first_.ptr());
-            if (f && THPVariable_Check(f)) {
-                const at::Tensor& t = THPVariable_Unpack(f);
-                if (t.dim() >= 1 && t.size(0) == 0) {
-                    n = 0;
-                    return true;
-                }
-            }
+        if (empty_shard(evidence, slots_, first_)) {
+            n = 0;
+            return true;
         }
         if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return false;
         n = c.n;
@@ -847,10 +891,7 @@ class FoldRing {
 
     Ops ops_;
     int G_;
-    bool eager_ = [] {
-        const char* e = getenv("CBN_FOLD_EAGER");
-        return e && e[0] == '1';
-    }();
+    bool eager_ = diag_switch("CBN_FOLD_EAGER");
     std::vector<Pending> cur_;
     std::deque<Group> exch_;
     std::deque<Pending> foldq_;
@@ -1016,15 +1057,9 @@ class FoldStepper {
 
   private:
     bool gather_cols(py::dict& evidence, Cols& c, int64_t& n) {
-        if (!first_.is_none()) {
-            PyObject* f = PyDict_GetItem(evidence.ptr(), first_.ptr());
-            if (f && THPVariable_Check(f)) {
-                const at::Tensor& t = THPVariable_Unpack(f);
-                if (t.dim() >= 1 && t.size(0) == 0) {
-                    n = 0;
-                    return true;
-                }
-            }
+        if (empty_shard(evidence, slots_, first_)) {
+            n = 0;
+            return true;
         }
         if (!gather(evidence, slots_, first_, dev_, target_observed_, c)) return false;
         n = c.n;
@@ -1159,6 +1194,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("nccl_unique_id", &nccl_unique_id);
     m.def("nccl_comm_init", &nccl_comm_init);
     m.def("nccl_comm_destroy", &nccl_comm_destroy);
+    m.def("nccl_comm_count", &nccl_comm_count);
     py::class_<Runner>(m, "Runner")
         .def(py::init<uintptr_t, uintptr_t, py::tuple, py::tuple, int64_t, int64_t, bool, uintptr_t, int32_t,
                       py::object>())

@@ -63,7 +63,10 @@ class Watchdog:
         self._armed = False
 
     def beat(self, **state):
-        self.state.update(state)
+        # copy-on-write: the watchdog thread's report() iterates whatever dict
+        # it read, never one being resized under it
+        if state:
+            self.state = {**self.state, **state}
         self._last = time.monotonic()
 
     def close(self):
@@ -76,7 +79,7 @@ class Watchdog:
         world = os.environ.get("WORLD_SIZE", "?")
         parts = [f"[cbn watchdog] rank {rank}/{world}: no progress for {time.monotonic() - self._last:.1f} s "
                  f"(bound {self.bound:.1f} s) {self.what}".rstrip(),
-                 "  state: " + ", ".join(f"{k}={v}" for k, v in self.state.items())]
+                 "  state: " + ", ".join(f"{k}={v}" for k, v in dict(self.state).items())]
         if self.describe is not None:
             try:
                 parts.append("  " + self.describe())
@@ -232,6 +235,8 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
 
 def _sharded_on_plan(eng, plan, fp, target_node, evidence_shard, N_max, group, gather, out, multi):
     n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
+    if n == 0:  # no launch checks an empty shard's columns: raise the reference's shape errors here
+        eng.check_columns(plan, evidence_shard)
     raw = eng.infer_raw(target_node, evidence_shard, N_max, out, fp=fp) if (fp is not None and n > 0) else None
     if raw is None and multi and fp is not None and fp.words is not None and n == 0:
         # an empty shard on a raw-capable plan: no rows, zero max words -- the
@@ -456,11 +461,11 @@ class ShardedStepper:
 
         res = native_step(evidence_shard)
         if res is None:  # dtype / device / layout the native checks reject: convert, same ring
+            # (shape errors first, as the reference raises them; no step is
+            # enqueued for a malformed batch)
+            eng.check_columns(fp.plan, evidence_shard)
             cols = {k: evidence_shard[k] for k in fp.slot_keys}
             conv = {k: v.to(device=fp.device, dtype=torch.float32).contiguous() for k, v in cols.items()}
-            for k, v in conv.items():
-                if v.dim() != 2:
-                    raise AssertionError("Each query tensor must be of dimension 2.")
             res = native_step(conv)
             if res is None:
                 raise ValueError("ShardedStepper.step: evidence batch rejected (shape / target-unobserved batch > 1)")
@@ -470,6 +475,15 @@ class ShardedStepper:
             _native.check(res, "cbn_plan_run(raw)")
         tdom = fp.tdom.get(res.shape[0])
         return res, (tdom if tdom is not None else self._tdom(fp, res.shape[0]))
+
+    def comm_ranks(self) -> Optional[int]:
+        """Ranks of the stepper's own RCCL communicator (ncclCommCount), None
+        before the first step or when the step uses none."""
+        if not self._comm:
+            return None
+        from . import _native
+
+        return int(_native.load_host().nccl_comm_count(self._comm))
 
     def describe(self) -> str:
         """One line of ring state for a watchdog report."""

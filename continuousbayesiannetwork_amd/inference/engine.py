@@ -615,12 +615,58 @@ class InferenceEngine:
             order = self._orders[target] = self.bn.get_ancestors(self.bn.initial_dag, target) + [target]
         return order
 
+    @staticmethod
+    def check_columns(plan: Plan, evidence):
+        """Raise what the reference raises for the plan's evidence columns, in
+        the reference's order: per factor (ancestors, target last), the
+        dimension / length asserts of Node.get_prob (node.py:127-135), then
+        the parents' columns in ``parents_names`` order -- a node whose sorted
+        evidence keys equal its ``parents_names`` copies each column into a
+        [Q, 1] slot (``new_query[:, i, :] = query[parent]``, :233-234), any
+        other node expands it to [Q, N] (``.expand(-1, N)``, :246-248): a
+        RuntimeError unless the width is 1 (or N for the expand).
+
+        A width-N column read only through ``.expand`` is accepted by the
+        reference as N per-sample values of the observed parent (a per-query
+        free parent); the kernels read element q of a column as query q's
+        value, so this engine raises NotImplementedError for it instead of
+        misreading it (Parity)."""
+        N = plan.n_samples
+        width_n = None
+        for spec in plan.factors:
+            if not spec.observed:
+                continue
+            cols = [evidence[p] for p in spec.observed]
+            n0 = cols[0].shape[0]
+            for t in cols:
+                assert t.shape[0] == n0, ValueError("n_queries must be equal for all features.")
+                assert t.dim() == 2, ValueError("Each query tensor must be of dimension 2.")
+            strict = sorted(spec.observed) == list(spec.parents)
+            for p in spec.observed:
+                t = evidence[p]
+                k = t.shape[1]
+                if k == 1:
+                    continue
+                if strict or k != N:
+                    target, shape = (1, f"[{n0}, 1]") if strict else (N, f"[-1, {N}]")
+                    raise RuntimeError(f"The expanded size of the tensor ({target}) must match the existing size "
+                                       f"({k}) at non-singleton dimension 1.  Target sizes: {shape}.  "
+                                       f"Tensor sizes: [{t.shape[0]}, {k}]")
+                width_n = width_n or p
+        if width_n is not None:
+            raise NotImplementedError(
+                f"evidence column {width_n!r} has shape [Q, {N}] (= N_max): the reference reads it as {N} "
+                f"per-sample values of a partially observed parent; this engine takes [n_queries, 1] evidence "
+                f"columns only")
+
     def _columns(self, plan: Plan, evidence, n_queries: int, device) -> List[torch.Tensor]:
         cols = []
         for v in plan.slots:
             t = evidence[v]
             assert t.dim() == 2, ValueError("Each query tensor must be of dimension 2.")
             assert t.shape[0] == n_queries, ValueError("n_queries must be equal for all features.")
+            if t.shape[1] != 1:
+                self.check_columns(plan, evidence)  # raises (the reference's error, in its order)
             if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
                 t = t.to(device=device, dtype=torch.float32).contiguous()
             cols.append(t)
@@ -868,7 +914,7 @@ class InferenceEngine:
         for i, v in enumerate(plan.slots):
             t = evidence[v]
             if (t.dtype is not torch.float32 or t.device != fp.device or t.dim() != 2 or t.shape[0] != n
-                    or not t.is_contiguous()):
+                    or t.shape[1] != 1 or not t.is_contiguous()):
                 return None  # slow path converts / raises the reference's errors
             ptrs[i] = t.data_ptr()
         if n == 0 or (not plan.target_observed and n != 1):

@@ -253,6 +253,14 @@ int32_t cbn_plan_flags(const cbn_plan* plan);
  * reporting path without starving the GPU).  No reference counterpart. */
 int cbn_debug_flag_timeout(cbn_plan* plan);
 
+/* 1 when the library was loaded with CBN_DIAG=1: only then are the
+ * diagnostic kernel-selection variables (CBN_NO_STAGED, CBN_FAST_VPL,
+ * CBN_PARAM_GENERIC, ... -- same-box A/B builds) honoured, and each CBN_*
+ * variable of the environment is listed on stderr at load.  Otherwise they
+ * are ignored: a stray variable cannot swap the kernels of a serving process.
+ * Added in round 5 (ABI 4, additive).  No reference counterpart. */
+int32_t cbn_diag_enabled(void);
+
 /* Average device time (ms) of the max and write passes over the timed calls
  * since the last read; waits for them; resets the ring. */
 int cbn_plan_timing(cbn_plan* plan, int32_t* n_timed, float* avg_max_ms, float* avg_write_ms);

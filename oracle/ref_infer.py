@@ -263,11 +263,13 @@ class OracleNode:
             if feats == self.parents:
                 q = np.zeros((n0, k, 1), np.float32)
                 for i, p in enumerate(self.parents):
+                    _check_width(query[p], 1, f"[{n0}, 1]")  # node.py:233-234 (a copy into [Q, 1])
                     q[:, i, :] = np.asarray(query[p], np.float32)
                 return q, q
             pts = np.empty((n0, k, N), np.float32)
             for i, p in enumerate(self.parents):
                 if p in feats:
+                    _check_width(query[p], N, f"[-1, {N}]")  # node.py:246-248 (.expand(-1, N))
                     pts[:, i, :] = np.broadcast_to(np.asarray(query[p], np.float32), (n0, N))
                 else:
                     pts[:, i, :] = self.sample_domain(p, N)[None, :]
@@ -278,6 +280,15 @@ class OracleNode:
                 pts[:, i, :] = self.sample_domain(p, N)[None, :]
             return self._meshgrid(pts), pts
         return None, None
+
+
+def _check_width(col: np.ndarray, target: int, shape: str):
+    """torch's broadcast error for an evidence column whose width is neither 1
+    nor ``target`` (the reference raises it from node.py:234 / :246-248)."""
+    k = col.shape[1]
+    if k != 1 and k != target:
+        raise RuntimeError(f"The expanded size of the tensor ({target}) must match the existing size ({k}) at "
+                           f"non-singleton dimension 1.  Target sizes: {shape}.  Tensor sizes: [{col.shape[0]}, {k}]")
 
 
 # --------------------------------------------------------------------------

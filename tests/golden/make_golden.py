@@ -148,6 +148,28 @@ CASES = [
          ev=["X0", "X1"], Q=24, N=6, ev_seed=306, seed=8),
     dict(name="cont4_free_support", data=("cont_free", 20000, 37), target="X3",
          ev=["X0", "X1"], Q=24, N=8, ev_seed=307, seed=9),
+    # evidence columns that are not [Q, 1] (round 5): width = {variable: k},
+    # column j of a widened variable drawn with ev_seed + 1000 j.  The
+    # reference copies a fully observed node's columns into [Q, 1] slots
+    # (node.py:233-234) and expands a partially observed node's to [Q, N]
+    # (:246-248): RuntimeError unless k = 1 (or k = N for the expand)
+    dict(name="err_width2_chain", data=("chain", 5, 4, 3000, 41), target="X4",
+         ev=["X0", "X1", "X2", "X3"], Q=16, N=4, ev_seed=401, expect_error=True,
+         width={"X0": 2, "X1": 2, "X2": 2, "X3": 2}),
+    dict(name="err_width2_last_slot", data=("chain", 5, 4, 3000, 42), target="X4",
+         ev=["X0", "X1", "X2", "X3"], Q=16, N=4, ev_seed=402, expect_error=True, width={"X3": 2}),
+    dict(name="err_width2_strict_parent", data=("multi", 2000, 43), target="E",
+         ev=["C", "A"], Q=12, N=3, ev_seed=403, expect_error=True, width={"A": 2}),
+    dict(name="err_width2_partial", data=("multi", 2000, 44), target="E",
+         ev=["C"], Q=12, N=3, ev_seed=404, expect_error=True, width={"C": 2}),
+    dict(name="err_width0", data=("chain", 5, 4, 3000, 45), target="X4",
+         ev=["X3"], Q=16, N=4, ev_seed=405, expect_error=True, width={"X3": 0}),
+    # ... and k = N through the expand only: the reference reads the column as
+    # N per-sample values of the observed parent (a per-query free parent);
+    # the HIP engine raises NotImplementedError for it (Parity),
+    # the oracle reproduces the values
+    dict(name="multi_widthN_partial", data=("multi", 2000, 46), target="E",
+         ev=["C"], Q=12, N=3, ev_seed=406, width={"C": 3}),
 ]
 
 
@@ -199,6 +221,9 @@ def main():
                              {"inference_obj": "exact"}, device="cpu")
         ev = sample_evidence(data, cols, c["ev"], c["Q"], seed=c.get("ev_seed", 100 + len(manifest)),
                              missing_frac=c.get("missing", 0.0))
+        for v, k in c.get("width", {}).items():
+            ev[v] = np.concatenate([sample_evidence(data, cols, [v], c["Q"], seed=c["ev_seed"] + 1000 * j)[v]
+                                    for j in range(k)], 1) if k > 0 else np.zeros((c["Q"], 0), np.float32)
         ev_t = {k: torch.tensor(v) for k, v in ev.items()}
         if c.get("evidence_none"):
             ev_t = None
@@ -213,11 +238,14 @@ def main():
             err = "AssertionError:" + str(e)
         except AttributeError as e:  # evidence=None (bayesian_network.py:193)
             err = "AttributeError:" + str(e)
+        except RuntimeError as e:  # an evidence column that is not [Q, 1] (node.py:233-248)
+            err = "RuntimeError:" + str(e)
         assert bool(err) == bool(c.get("expect_error", False)), (c["name"], err)
         out = dict(data=data.astype(np.float32), pdf=pdf, domain=dom,
                    meta=np.array(json.dumps(dict(
                        name=c["name"], columns=cols, edges=edges, target=c["target"],
-                       evidence=list(ev.keys()), evidence_none=bool(c.get("evidence_none")), N_max=c["N"], seed=seed, error=err))))
+                       evidence=list(ev.keys()), evidence_none=bool(c.get("evidence_none")), N_max=c["N"], seed=seed, error=err,
+                       width=c.get("width", {})))))
         for k, v in ev.items():
             out["ev_" + k] = v
         np.savez_compressed(os.path.join(HERE, c["name"] + ".npz"), **out)

@@ -20,6 +20,22 @@ def load_golden(name):
     return dict(meta=meta, data=z["data"], pdf=z["pdf"], domain=z["domain"], evidence=ev)
 
 
+ERRORS = {"AttributeError": AttributeError, "AssertionError": AssertionError, "RuntimeError": RuntimeError}
+
+
+def golden_error(meta):
+    """(exception type, message) of a fixture whose reference run raised."""
+    kind, _, msg = meta["error"].partition(":")
+    return ERRORS[kind], msg
+
+
+def width_n_only(meta):
+    """A fixture whose evidence has [Q, N] columns that the reference reads
+    through ``.expand(-1, N)`` only (node.py:246-248) -- accepted by the
+    reference, NotImplementedError in the HIP engine (Parity)."""
+    return not meta["error"] and any(k != 1 for k in meta.get("width", {}).values())
+
+
 def param_golden_names():
     with open(os.path.join(GOLDEN_DIR, "MANIFEST_param.json")) as f:
         return json.load(f)["cases"]

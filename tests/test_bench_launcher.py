@@ -67,6 +67,11 @@ def test_n_gt_1_value_is_the_gathered_step():
     assert m["sharded"] and not m["gather"] and m["fold"]
     p = bench.projection(8)
     assert p["gathered_x_vs_1gpu"] < 2.0 < p["rank_local_x_vs_1gpu"]
+    # the communicator's rank count must equal --gpus
+    assert bench.multi_gpu_fields(2, 2, 2)["rccl_ranks"] == 2
+    assert bench.multi_gpu_fields(1, 1, None) == {"rccl_ranks": None}
+    with pytest.raises(SystemExit, match="communicator has 1 ranks"):
+        bench.multi_gpu_fields(2, 2, 1)
 
 
 STANDIN_MODES = """
@@ -77,6 +82,11 @@ world = bench.check_world(2, os.environ)
 m = bench.step_modes(bench.parse(["--gpus", "2"]), world)
 line = {{"n_gpus": world, "value_kind": m["value_kind"], "config": {{"parallelism": m["parallelism"]}}}}
 line["value_" + m["other_kind"]] = 1.0
+# the stepper's RCCL communicator is stood in for by the gloo group's size
+import torch.distributed as dist
+dist.init_process_group("gloo")
+line.update(bench.multi_gpu_fields(2, world, dist.get_world_size()))
+dist.destroy_process_group()
 open(os.path.join(sys.argv[1], "line" + os.environ["RANK"]), "w").write(json.dumps(line))
 """
 
@@ -95,6 +105,10 @@ def test_two_rank_launch_line_names_the_all_gather(tmp_path):
         line = json.loads((tmp_path / f"line{r}").read_text())
         assert line["n_gpus"] == 2 and line["value_kind"] == "gathered"
         assert "all-gather" in line["config"]["parallelism"] and "value_rank_local" in line
+        assert line["rccl_ranks"] == 2
+        p = line["projection"]
+        assert p["link_assumption"].startswith("assumed") and "not a measurement" in p["status"]
+        assert p["gathered_x_vs_1gpu_if_bidirectional"] <= p["gathered_x_vs_1gpu"]
 
 
 STANDIN_STALL = """

@@ -314,6 +314,14 @@ class _OracleEngine:
         return torch.tensor(raw), torch.tensor(dom)
 
     @staticmethod
+    def check_columns(plan, ev):
+        """InferenceEngine.check_columns raises the reference's shape errors
+        for an empty shard (no launch checks it); the stand-in's shards are
+        well-formed [Q, 1] columns."""
+        for v in ev.values():
+            assert v.dim() == 2 and v.shape[1] == 1
+
+    @staticmethod
     def _bits(rows):
         m = float(rows.max()) if rows.numel() else 0.0
         return torch.tensor([np.float32(m).view(np.int32)], dtype=torch.int32)

@@ -264,3 +264,75 @@ def test_native_runner_path_matches_and_falls_back(gpu):
     np.testing.assert_allclose(got.cpu().numpy(), ref2, rtol=RTOL, atol=ATOL)
     got2, _ = bn.infer("X7", dict(ev), N_max=8)  # the rebuilt plan's runner
     np.testing.assert_array_equal(got2.cpu().numpy(), got.cpu().numpy())
+
+
+def test_evidence_width_raises_like_the_reference(gpu):
+    """An evidence column that is not [Q, 1] raises the reference's RuntimeError
+    (node.py:233-234 copies a fully observed node's columns into [Q, 1] slots;
+    :246-248 expands a partially observed node's to [Q, N]) on every path --
+    the first (planning) call, a repeat call after valid ones (the native
+    Runner declines it), infer_raw, sharded_infer and ShardedStepper.step,
+    empty shards included -- instead of the kernels reading element q of a
+    wider tensor as query q's value.  A strided [Q, 1] view (x[:, 1:2] of a
+    [Q, 3] tensor) is still a valid column and matches the oracle."""
+    import re
+
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper, sharded_infer
+
+    data, cols, edges = chain_data(8, 8, 5000, 4, stay=0.7)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    eng = bn.engine
+    names = [c for c in cols if c != "X7"]
+    ev = _t(sample_evidence(data, cols, names, 777, 2), gpu)
+    msg = re.escape("The expanded size of the tensor (1) must match the existing size (2) at non-singleton "
+                    "dimension 1.  Target sizes: [777, 1].  Tensor sizes: [777, 2]")
+    wide = dict(ev)
+    wide["X6"] = torch.cat([ev["X6"], ev["X5"]], 1).contiguous()
+    with pytest.raises(RuntimeError, match=msg):  # first call: plans, then the general path
+        bn.infer("X7", wide, N_max=8)
+    a, _ = bn.infer("X7", ev, N_max=8)
+    a2, _ = bn.infer("X7", ev, N_max=8)
+    assert eng._runner is not None
+    for _ in range(2):  # the runner path declines, the general path raises
+        with pytest.raises(RuntimeError, match=msg):
+            bn.infer("X7", dict(wide), N_max=8)
+    first = dict(ev)
+    first["X0"] = torch.cat([ev["X0"]] * 3, 1)
+    with pytest.raises(RuntimeError, match=re.escape("existing size (3)")):
+        bn.infer("X7", first, N_max=8)
+    zero = dict(ev)
+    zero["X3"] = ev["X3"][:, :0]
+    with pytest.raises(RuntimeError, match=re.escape("existing size (0)")):
+        bn.infer("X7", zero, N_max=8)
+    # strided [Q, 1] views of [Q, 3] tensors are valid columns
+    strided = {k: torch.cat([v + 100, v, v - 100], 1)[:, 1:2] for k, v in ev.items()}
+    assert not strided["X6"].is_contiguous() and strided["X6"].shape == (777, 1)
+    s1, _ = bn.infer("X7", strided, N_max=8)
+    np.testing.assert_array_equal(s1.cpu().numpy(), a.cpu().numpy())
+    ref, _ = OracleBN(edges, cols, data).infer("X7", {k: v.cpu().numpy() for k, v in ev.items()}, 8)
+    np.testing.assert_allclose(s1.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    # the raw launch and the sharded paths
+    with pytest.raises(RuntimeError, match=msg):
+        eng.infer_raw("X7", wide, 8)
+    with pytest.raises(RuntimeError, match=msg):
+        sharded_infer(bn, "X7", wide, 8)
+    empty_wide = {k: v[:0] for k, v in wide.items()}
+    with pytest.raises(RuntimeError, match=re.escape("existing size (2)")):
+        sharded_infer(bn, "X7", empty_wide, 8)
+    for fold in (False, True):
+        st = ShardedStepper(bn, "X7", 8, exchange_every=2, fold=fold)
+        r, _ = st.step(ev)
+        with pytest.raises(RuntimeError, match=msg):
+            st.step(wide)
+        with pytest.raises(RuntimeError, match=re.escape("existing size (2)")):
+            st.step(empty_wide)
+        r2, _ = st.step(strided)
+        st.wait()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(r.cpu().numpy(), a.cpu().numpy())
+        np.testing.assert_array_equal(r2.cpu().numpy(), a.cpu().numpy())
+        st.close()
+    np.testing.assert_array_equal(a2.cpu().numpy(), a.cpu().numpy())
+    # the Node.get_prob mirror raises the same way (node.py:233-234)
+    with pytest.raises(RuntimeError):
+        bn.nodes_obj["X7"].get_prob({"X6": wide["X6"]}, 8)

@@ -18,7 +18,7 @@ import pytest
 import torch
 
 from continuousbayesiannetwork_amd import BayesianNetwork, BruteForce, _native
-from golden_io import golden_names, load_golden
+from golden_io import golden_names, load_golden, width_n_only
 from helpers import continuous_free_data, hicard_data, make_bn, sample_evidence, wide_data
 from oracle.ref_infer import OracleBN, OracleBruteForce
 
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 RTOL, ATOL = 1e-5, 1e-7
 DIRECT_GOLDENS = ["wide10_free2", "wide12_all", "hicard40_all", "hicard40_free1", "cont4_all", "cont4_free1",
                   "cont4_free_support"]
-OK_GOLDENS = [n for n in golden_names() if not load_golden(n)["meta"]["error"]]
+OK_GOLDENS = [n for n in golden_names() if not load_golden(n)["meta"]["error"] and not width_n_only(load_golden(n)["meta"])]
 
 
 def _t(ev, dev):
@@ -187,7 +187,8 @@ def test_direct_free_combos_beyond_2_20_and_the_call_bound(gpu):
     round 4 by a fixed 2^20 cap) -- it now runs, and its free-parent mean
     matches an fp64 numpy evaluation of the fitted CPD; a call whose work
     (queries x columns x combos) exceeds 2^40 CPD lookups is refused with
-    NativeError (CBN_E_LIMIT) before anything launches."""
+    NativeError (CBN_E_LIMIT) before anything launches, and so is a plan whose
+    (query, column) threads would each loop over more than 2^26 combos."""
     S, k, d = 200_000, 7, 16
     rng = np.random.default_rng(11)
     P = rng.integers(0, d, (S, k))
@@ -223,3 +224,9 @@ def test_direct_free_combos_beyond_2_20_and_the_call_bound(gpu):
     big = {"P0": torch.full((8192, 1), 3.0, device=gpu)}
     with pytest.raises(_native.NativeError, match="split the batch"):
         bn.infer("Y", big, N_max=d)
+    # the per-thread bound: without evidence Y's factor averages
+    # 16^7 = 2^28 combos per column in ONE thread's serial loop -- refused at
+    # plan creation whatever the batch (a one-query call is no shorter)
+    bn.engine.force_direct = True
+    with pytest.raises(_native.NativeError, match=r"2\^26"):
+        bn.infer("Y", {}, N_max=d)

@@ -412,27 +412,6 @@ def test_parametric_sharded_stepper_equals_infer(gpu):
     st.close()
 
 
-def test_generic_kernel_equals_fast_kernel(gpu, monkeypatch):
-    """The generic kernel (forced by CBN_PARAM_GENERIC) runs the fast kernels'
-    operations in the same order: bit-identical rows on an NN [16] network
-    with free parents."""
-    data, cols, edges = mixed_dag_data(3000, 4, n=12, unit=True)
-    model = {"hidden_dims": [16], "activation": "tanh"}
-    names = [cols[-2], cols[5], cols[2]]
-    ev = _t(sample_evidence(data, cols, names, 500, 3), gpu)
-    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu, estimator="neural_network",
-                 config=param_config("neural_network", n_epochs=10, model=model))
-    monkeypatch.setenv("CBN_PARAM_PARTS", "1")  # one factor range per wave: the generic kernel's product order
-    outs = []
-    for generic in (False, True):
-        if generic:  # read at plan creation: drop the cached plan
-            monkeypatch.setenv("CBN_PARAM_GENERIC", "1")
-            bn.engine.invalidate()
-        random.seed(4)
-        outs.append(bn.infer(cols[-1], ev, N_max=8)[0].cpu().numpy())
-    np.testing.assert_array_equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("observed", [10, 8])
 def test_ten_parent_parametric_node(observed, gpu):
     """A LinearRegression node with 10 parents (beyond the fixed input array):

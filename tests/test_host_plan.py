@@ -8,8 +8,8 @@ import torch
 
 from continuousbayesiannetwork_amd import BayesianNetwork
 from continuousbayesiannetwork_amd._native import CBN_FACTOR_QUERY, CBN_FACTOR_SCALAR, CBN_FACTOR_SHARED
-from continuousbayesiannetwork_amd.inference.engine import build_factor_specs, relevant_observed
-from golden_io import golden_names, load_golden
+from continuousbayesiannetwork_amd.inference.engine import InferenceEngine, Plan, build_factor_specs, relevant_observed
+from golden_io import golden_error, golden_names, load_golden
 from helpers import make_bn
 from oracle.ref_infer import OracleBN
 
@@ -151,3 +151,32 @@ def test_redraw_program_mixed_cards():
     data[:, 2] = np.round(data[:, 2] * 4) % 2  # a binary column among 5-level ones
     for N in (3, 5, 8):
         _redraw_case(edges, cols, data, "X5", ["X1", "X3"], N, seeds=(1, 2))
+
+
+@pytest.mark.parametrize("name", [n for n in golden_names() if load_golden(n)["meta"].get("width")])
+def test_evidence_width_checks_match_reference(name):
+    """Evidence columns that are not [Q, 1] (reference fixtures
+    err_width*, multi_widthN_partial): InferenceEngine.check_columns raises the
+    reference's RuntimeError with its message (node.py:233-234, 246-248) --
+    or NotImplementedError for the [Q, N] column the reference reads as N
+    per-sample values.  Host logic only: the plan's factor specs, no launch."""
+    g = load_golden(name)
+    m = g["meta"]
+    bn = make_bn(BayesianNetwork, m["edges"], m["columns"], g["data"], device="cpu")
+    ev = {k: torch.tensor(g["evidence"][k]) for k in m["evidence"]}
+    order = bn.get_ancestors(bn.initial_dag, m["target"]) + [m["target"]]
+    obs = relevant_observed(bn, order, ev.keys())
+    random.seed(m["seed"])
+    order, specs, tdom, det = build_factor_specs(bn, m["target"], obs, m["N_max"])
+    plan = Plan(m["target"], m["N_max"], order, specs, sorted(obs), tdom, True, det)
+    if m["error"]:
+        exc, msg = golden_error(m)
+        with pytest.raises(exc) as info:
+            InferenceEngine.check_columns(plan, ev)
+        assert str(info.value) == msg
+    else:
+        with pytest.raises(NotImplementedError):
+            InferenceEngine.check_columns(plan, ev)
+    # the same columns at width 1 pass
+    InferenceEngine.check_columns(plan, {k: v[:, :1] if v.shape[1] else torch.zeros((v.shape[0], 1))
+                                         for k, v in ev.items()})

@@ -149,3 +149,49 @@ def test_sparse_conditionals_match_oracle_rows():
     np.testing.assert_allclose(vals, ref, rtol=1e-6, atol=0)
     assert len(np.unique(cell)) == len(cell)
     assert hash_capacity(len(cell)) >= 2 * len(cell) and hash_capacity(1) == 2 and hash_capacity(5) == 16
+
+
+def test_diagnostic_switches_need_cbn_diag():
+    """Kernel-selection switches (CBN_NO_STAGED, CBN_PARAM_GENERIC, ...) count
+    only when the library is loaded with CBN_DIAG=1 (cbn_diag_enabled), which
+    then lists every CBN_* override on stderr; a stray CBN_NO_STAGED=1 alone is
+    ignored (the GPU side, tests/test_gpu_diag.py, checks the plan flags)."""
+    import json
+    import subprocess
+    import sys
+
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "diag_child.py")
+    base = {k: v for k, v in os.environ.items() if not k.startswith("CBN_")}
+
+    def run(**env):
+        p = subprocess.run([sys.executable, child, "enabled"], env={**base, **env}, capture_output=True, text=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        return json.loads(p.stdout.strip().splitlines()[-1])["diag"], p.stderr
+
+    d, err = run(CBN_NO_STAGED="1")
+    assert d == 0 and "diagnostic override" not in err
+    d, err = run(CBN_DIAG="1", CBN_NO_STAGED="1", CBN_FAST_VPL="1")
+    assert d == 1
+    assert "diagnostic override CBN_NO_STAGED=1" in err and "diagnostic override CBN_FAST_VPL=1" in err
+    d, _ = run(CBN_DIAG="0", CBN_NO_STAGED="1")
+    assert d == 0
+
+
+def test_runner_key_whose_eq_raises_falls_back():
+    """A dict key whose __eq__ raises: the Runner's key walk
+    clears the error and declines the call (None) instead of leaving a Python
+    exception set behind its return value."""
+    import torch
+
+    class Key(str):
+        def __eq__(self, other):
+            raise ValueError("no comparison")
+
+        __hash__ = str.__hash__
+
+    host = _native.load_host()
+    tdom = torch.zeros(4)
+    r = host.Runner(0, 0, ("a",), ("a",), 0, 4, True, 0, 0, tdom)
+    assert r({Key("b"): torch.zeros(8, 1)}, None) is None
+    assert r({"a": torch.zeros(8, 1)}, None) is None  # a CPU column: declined too

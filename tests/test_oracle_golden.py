@@ -7,7 +7,7 @@ import random
 import numpy as np
 import pytest
 
-from golden_io import golden_names, load_golden, load_param_golden, oracle_estimators, param_golden_names
+from golden_io import golden_error, golden_names, load_golden, load_param_golden, oracle_estimators, param_golden_names
 from oracle.ref_infer import OracleBN
 
 RTOL, ATOL = 1e-5, 1e-7
@@ -21,11 +21,13 @@ def test_oracle_matches_reference_golden(name):
     random.seed(m["seed"])
     ev = None if m["evidence_none"] else {k: g["evidence"][k] for k in m["evidence"]}
     if m["error"]:
-        exc = AttributeError if m["error"].startswith("AttributeError") else AssertionError
-        with pytest.raises(exc):
+        exc, msg = golden_error(m)
+        with pytest.raises(exc) as info:
             if ev is None:
                 ev.items()
             bn.infer(m["target"], ev, m["N_max"])
+        if exc is RuntimeError:  # the evidence-width errors: the reference's message too
+            assert str(info.value) == msg
         return
     pdf, dom = bn.infer(m["target"], ev, m["N_max"])
     assert pdf.shape == g["pdf"].shape

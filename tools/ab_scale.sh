@@ -3,6 +3,7 @@
 # tools/ab_scale.sh 1 2 4 ...  -> bench.py --sharded (N = 1 over a one-rank RCCL
 # communicator), two rounds, per-step time and the raw launch's HIP-event time
 set -u
+export CBN_DIAG=1  # diagnostic CBN_* switches count only under CBN_DIAG=1 (round 5)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 for round in 1 2; do

@@ -3,6 +3,7 @@
 # folded scales vs the separate batched scale (new: 1 block/CU, 8 float4 per
 # thread in flight; old: 4 blocks/CU, one float4 per thread)
 set -u
+export CBN_DIAG=1  # diagnostic CBN_* switches count only under CBN_DIAG=1 (round 5)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export MASTER_ADDR=127.0.0.1 MASTER_PORT=29533

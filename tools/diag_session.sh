@@ -4,6 +4,7 @@
 # Build first (here, on the CPU): tools/build_variant.sh stamps -DCBN_STAMPS,
 # tools/build_variant.sh abl_<X> -DCBN_ABL_<X> ..., hipcc tools/probes/ramp.hip.
 set -u
+export CBN_DIAG=1  # diagnostic CBN_* switches count only under CBN_DIAG=1 (round 5)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,6 +1,7 @@
 #!/bin/bash
 # quick GPU iteration: parity subset, bench, stamps
 set -u
+export CBN_DIAG=1  # diagnostic CBN_* switches count only under CBN_DIAG=1 (round 5)
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
