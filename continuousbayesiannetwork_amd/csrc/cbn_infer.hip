@@ -883,10 +883,21 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
             // flight before their products (memory-level parallelism for the
             // gather), multiplied in factor order
             constexpr int KB = VPL == 2 ? 6 : 8;  // 48 / 32 VGPRs of rows in flight (8 at VPL 2 spills)
+            // Zero-product skip (round 5): table entries are finite and >= 0
+            // (BruteForce conditionals and their free-parent means), so once
+            // every accumulator of a lane is +0 no later factor can change that
+            // lane's outputs -- its remaining row gathers are masked off (the
+            // products then multiply +0 by +0: the same bits).  On the
+            // configs[4] peaked grid the median lane is all-zero after 4 of
+            // 100 factors and 84 % of the gathers are skippable per lane, none
+            // per wave (62 % of queries keep a nonzero column):
+            // profiles/r05_zero_histogram.json.
+            bool alive = true;
             for (int f0 = 0; f0 < nf; f0 += KB) {
+                if (__builtin_amdgcn_ballot_w64(alive) == 0) break;  // every lane of the wave is all-zero
                 int oo[KB];
 #pragma unroll
-                for (int k = 0; k < KB; ++k) oo[k] = f0 + k < nf ? my[f0 + k] : -1;
+                for (int k = 0; k < KB; ++k) oo[k] = (f0 + k < nf && alive) ? my[f0 + k] : -1;
                 float4 t[KB][VPL];
 #pragma unroll
                 for (int k = 0; k < KB; ++k) {
@@ -917,6 +928,10 @@ k_query_fast(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
                         }
                     }
                 }
+                bool nz = false;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) nz |= acc[i] != 0.f;  // (NaN counts as alive)
+                alive = nz;
             }
         } else if (pr) {
             // factor pairs (f, f + 1) in bank halves 0 / 1: four reads per pair,

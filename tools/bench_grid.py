@@ -16,7 +16,8 @@ from the plan image (85 MB: beyond the 32 MiB of L2, inside the 256 MiB
 Infinity Cache); the gather rate is compared with the guide's gather
 figures: rows shared through an XCD's L2 16.8-18.8 TB/s, uniformly random
 rows of a 38 MB table (Infinity Cache) 8.6 TB/s (MI355X_MICROARCH.md
-'Indexed rows').  ``--profile``: one workload, 10 calls (for rocprofv3)."""
+'Indexed rows').  ``--profile``: one workload, 10 calls (for rocprofv3);
+``--headline``: the peaked network only (A/B sessions)."""
 import json
 import os
 import sys
@@ -33,7 +34,7 @@ from helpers import grid_data, make_bn, sample_evidence  # noqa: E402
 
 def main():
     prof = "--profile" in sys.argv
-    cases = ((0.995, 0),) if prof else ((0.995, 0), (0.8, 2))
+    cases = ((0.995, 0),) if prof or "--headline" in sys.argv else ((0.995, 0), (0.8, 2))
     for keep, noise in cases:
         run(keep, noise, prof)
 

@@ -15,6 +15,8 @@
 #   prof          rocprofv3 --kernel-trace --stats of the driver's command
 #   pmcNAME       one rocprofv3 --pmc pass of the driver's command with the counters in $PMC_NAME
 #   stamps        tools/stamp_probe.py (per-wave phase stamps, configs[1])
+#   ab            A/B of library variants (AB_LIBS="base old", libcbn_amd_<name>.so built by
+#                 tools/build_variant.sh) on tools/bench_$AB_BENCH.py (default grid), two rounds
 # Diagnostic kernel-selection variables (CBN_NO_STAGED, ...) need CBN_DIAG=1
 # in the environment of the session (include/cbn_amd.h, cbn_diag_enabled).
 set -u
@@ -59,6 +61,16 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc $counters -d $O/pmc_$name -o run -- python3 bench.py --gpus 1 --steps 20 \
         --warmup 5 --no-cpu-baseline > $O/pmc_$name.json 2> $O/pmc_$name.err || exit $?
       find $O/pmc_$name -name "*counter_collection.csv" | head -2 ;;
+    ab)  # same-box A/B of library variants on tools/bench_$AB_BENCH.py, two rounds (base = the in-tree library)
+      for r in 1 2; do
+        for v in ${AB_LIBS:-base old}; do
+          if [ $v = base ]; then lib=$PWD/continuousbayesiannetwork_amd/libcbn_amd.so
+          else lib=$PWD/continuousbayesiannetwork_amd/libcbn_amd_$v.so; fi
+          CBN_LIB_PATH=$lib timeout -k 10 600 python3 tools/bench_${AB_BENCH:-grid}.py ${BENCH_ARGS:-} \
+            > $O/ab_${v}_$r.log 2>&1 || exit $?
+          grep '^{' $O/ab_${v}_$r.log | cut -c1-300 | sed "s/^/$v $r /"
+        done
+      done ;;
     stamps)
       timeout -k 10 300 python3 tools/stamp_probe.py > $O/stamps.log 2>&1 || exit $?
       tail -20 $O/stamps.log ;;

@@ -15,7 +15,12 @@ lib = nat.load()
 lib.cbn_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
 S = 12
 buf = torch.zeros(4096 * 16 * S, dtype=torch.int64, device=dev)
-if os.environ.get("ALARM"):  # BASELINE configs[2]: k_query_fast on global tables (tools/bench_alarm.py)
+nat.LIB_PATH = os.environ.get("CBN_LIB_PATH", nat.LIB_PATH)
+if os.environ.get("GRID"):  # BASELINE configs[4]: peaked 10 x 10 grid, k_query_fast on global tables
+    from helpers import grid_data
+    data, cols, edges = grid_data(400_000, 3, side=10, d=64, keep=0.995, noise=0)
+    target, Q, NM = "X99", 65536, 64
+elif os.environ.get("ALARM"):  # BASELINE configs[2]: k_query_fast on global tables (tools/bench_alarm.py)
     from helpers import alarm_like_data
     data, cols, edges = alarm_like_data(200_000, 5)
     target, Q, NM = "X35", 262144, 8
@@ -48,6 +53,9 @@ for k in range(1, 11):
     print(f"  d{k:<2} {names[k]:28s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}  max {d.max():9.0f}")
 tot = st[:, 10] - st[:, 0] if bn.engine.fused else st[:, 7] - st[:, 0]
 tot = tot[tot > 0]
+if tot.size == 0:  # (no post-barrier stamps: entry -> loop end)
+    tot = st[:, 7] - st[:, 0]
+    tot = tot[tot > 0]
 print("  total per wave: median", np.median(tot), "max", tot.max(), "(units: 10 ns ticks of s_memrealtime)")
 # launch / arrival skew within each XCD (blocks b and b+8 share an XCD, so their s_memtime is comparable)
 full = buf.view(-1, 16, S).cpu().numpy()  # [block, wave, stamp]
