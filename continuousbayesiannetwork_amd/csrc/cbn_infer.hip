@@ -174,8 +174,19 @@ __device__ __forceinline__ unsigned wave_max_u(unsigned v) {
 __device__ unsigned long long* g_stamps = nullptr;
 // the buffer pointer is read ONCE per wave (CBN_STAMP_INIT, after stamp 0's
 // clock read); a stamp is then one s_memrealtime + one un-waited store
+// Clock ring (round 5): per launch of k_query_staged,
+// block 0 / thread 0 records {shader cycles (s_memtime), 100 MHz ticks
+// (s_memrealtime)} at entry and after its final stores -- block 0 waits in the
+// grid barrier for every other block, so its span is the launch's, and the
+// ratio of the two is the shader clock the launch ran at.  Plain vector
+// stores by one lane; launches on one stream run one after the other.
+constexpr unsigned kClockRing = 4096;
+__device__ unsigned long long* g_clock = nullptr;  // [launch][4]
+__device__ unsigned g_clock_n = 0;
 #define CBN_STAMP_INIT                                                                        \
     const unsigned long long _t0 = __builtin_amdgcn_s_memrealtime();                          \
+    const unsigned long long _m0 = __builtin_amdgcn_s_memtime();                              \
+    (void)_m0;                                                                                \
     unsigned long long* const _stp = g_stamps;                                                \
     if (_stp && (threadIdx.x & 63) == 0)                                                      \
         _stp[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12] = _t0
@@ -187,9 +198,26 @@ __device__ unsigned long long* g_stamps = nullptr;
             _stp[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 12 + (k)] = _t; \
         __builtin_amdgcn_sched_barrier(0);                                                    \
     } while (0)
+#define CBN_CLOCK_END                                                                         \
+    do {                                                                                      \
+        unsigned long long* const _ck = g_clock;                                              \
+        if (_ck && blockIdx.x == 0 && threadIdx.x == 0) {                                     \
+            const unsigned long long _m1 = __builtin_amdgcn_s_memtime();                      \
+            const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();                  \
+            const unsigned _i = g_clock_n;                                                    \
+            if (_i < kClockRing) {                                                            \
+                _ck[4 * _i] = _m0;                                                            \
+                _ck[4 * _i + 1] = _t0;                                                        \
+                _ck[4 * _i + 2] = _m1;                                                        \
+                _ck[4 * _i + 3] = _r1;                                                        \
+            }                                                                                 \
+            g_clock_n = _i + 1;                                                               \
+        }                                                                                     \
+    } while (0)
 #else
 #define CBN_STAMP_INIT do {} while (0)
 #define CBN_STAMP(k) do {} while (0)
+#define CBN_CLOCK_END do {} while (0)
 #endif
 
 // Diagnostic build only (-DCBN_CHECKED): validate global addresses in the
@@ -1784,6 +1812,7 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
             store_wt(orsrc, ob + chi * 4, make_float4(o[4], o[5], o[6], o[7]));
         }
         CBN_STAMP(10);
+        CBN_CLOCK_END;
     }
 }
 
@@ -2148,6 +2177,15 @@ int cbn_debug_flag_timeout(cbn_plan* plan) {
 
 int cbn_debug_set_stamp_buffer(void* dev_ptr) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(void*)));
+    return CBN_OK;
+}
+
+// the clock ring of k_query_staged (CBN_CLOCK_END): dev_ptr = [kClockRing][4]
+// unsigned long long (nullptr: off); resets the launch counter
+int cbn_debug_set_clock_buffer(void* dev_ptr) {
+    const unsigned zero = 0;
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_clock), &dev_ptr, sizeof(void*)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_clock_n), &zero, sizeof(zero)));
     return CBN_OK;
 }
 #endif

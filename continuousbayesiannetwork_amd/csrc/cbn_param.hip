@@ -608,17 +608,136 @@ __device__ __forceinline__ void add_row_t(float (&fx)[NC], float (&cx)[NC], cons
     }
 }
 
-// acc[j] *= pdf(S[j]; mu): the M == 1 factor (a mean over size-1 axes is the pdf itself)
+#ifndef CBN_MULROW_GROUP
+#define CBN_MULROW_GROUP 8
+#endif
+// pdf2_t's fast form on NP column pairs at once -- every wave-uniform
+// fall-back of exp_split2 / exp_neg_half2 / div_nr2 assumed not taken -- plus
+// what decides it: lo = the smallest x log2(e) of the exponentials (their
+// fall-back: < -126), bad = a division whose fall-back (denominator > 2^126,
+// inf or NaN) some lane needs.  Where neither is set the fast form IS
+// pdf2_t, operation for operation.  Written step by step across the pairs
+// (every pair's t, then every pair's t^2, ...): independent packed ops back
+// to back, so the packed-math hazard nops of one pair's dependent chain are
+// filled by the other pairs' work.
+template <int NP, int MODE>
+__device__ __forceinline__ void pdf2_fast(float scale, float inv_scale, float norm, const float* sv, float mu,
+                                          f2 (&out)[NP], float& lo, bool& bad) {
+#pragma clang fp contract(off)
+    constexpr float kL = 1.44269502162933349609375f;
+    constexpr float kLlo = 1.925963033500e-8f;
+    constexpr float kLn2 = 0.693147180559945309f;
+    f2 t[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) t[k] = f2{sv[2 * k], sv[2 * k + 1]} - f2s(mu);
+    if (MODE == 1 || MODE == 3) {  // div_nr2 by the scale (uniform)
+        f2 q[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) q[k] = t[k] * f2s(inv_scale);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) t[k] = fma2(fma2(-f2s(scale), q[k], t[k]), f2s(inv_scale), q[k]);
+        bad |= !(scale <= 0x1p126f);
+    }
+    f2 a[NP], ph[NP], pl[NP], r[NP];
+    if (MODE <= 1) {  // exp_neg_half2(t * t)
+        constexpr float kHL = -0.5f * kL, kHLlo = -0.5f * kLlo;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) a[k] = t[k] * t[k];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) ph[k] = a[k] * f2s(kHL);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) r[k] = f2{__builtin_amdgcn_exp2f(ph[k].x), __builtin_amdgcn_exp2f(ph[k].y)};
+#pragma unroll
+        for (int k = 0; k < NP; ++k) pl[k] = fma2(a[k], f2s(kHL), -ph[k]);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) pl[k] = fma2(a[k], f2s(kHLlo), pl[k]);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) lo = fminf(lo, fminf(ph[k].x, ph[k].y));
+#pragma unroll
+        for (int k = 0; k < NP; ++k) pl[k] = pl[k] * f2s(kLn2);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) r[k] = fma2(r[k], pl[k], r[k]);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) out[k] = f2s(norm) * r[k];
+        return;
+    }
+    // exp_split2(-t), then div_nr2(e, u^2 [* scale])
+#pragma unroll
+    for (int k = 0; k < NP; ++k) a[k] = -t[k];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) ph[k] = a[k] * f2s(kL);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) r[k] = f2{__builtin_amdgcn_exp2f(ph[k].x), __builtin_amdgcn_exp2f(ph[k].y)};
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pl[k] = fma2(a[k], f2s(kL), -ph[k]);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pl[k] = fma2(a[k], f2s(kLlo), pl[k]);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) lo = fminf(lo, fminf(ph[k].x, ph[k].y));
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pl[k] = pl[k] * f2s(kLn2);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) r[k] = fma2(r[k], pl[k], r[k]);  // e
+#pragma unroll
+    for (int k = 0; k < NP; ++k) a[k] = f2s(1.f) + r[k];  // u
+#pragma unroll
+    for (int k = 0; k < NP; ++k) a[k] = MODE == 2 ? a[k] * a[k] : f2s(scale) * (a[k] * a[k]);  // d
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        ph[k] = f2{__builtin_amdgcn_rcpf(a[k].x), __builtin_amdgcn_rcpf(a[k].y)};
+        bad |= !(a[k].x <= 0x1p126f) || !(a[k].y <= 0x1p126f);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pl[k] = r[k] * ph[k];  // q
+#pragma unroll
+    for (int k = 0; k < NP; ++k) out[k] = fma2(fma2(-a[k], pl[k], r[k]), ph[k], pl[k]);
+}
+
+// acc[j] *= pdf(S[j]; mu): the M == 1 factor (a mean over size-1 axes is the
+// pdf itself).  Round 5: the NC sample values are read first (one scalar-load
+// burst, one wait) and every column pair runs the fast form straight through
+// (no per-pair branch, so the compiler interleaves the pairs and the
+// packed-math hazard nops disappear); one wave-uniform test per 8 columns
+// decides whether some lane needed a fall-back of pdf2_t in one of their pairs
+// -- then those pairs are redone by pdf2_t itself.  Either way every product is
+// pdf2_t's, so the bits are those of the per-pair form.
 template <int NC, int MODE>
 __device__ __forceinline__ void mul_row_t(float (&acc)[NC], const float* __restrict__ S, float sc, float isc,
                                           float nm, float mu) {
     static_assert(NC % 2 == 0, "column pairs");
+#if CBN_MULROW_GROUP == 0  // diagnostic A/B: the per-pair form
 #pragma unroll
     for (int j = 0; j < NC; j += 2) {
         const f2 r = f2{acc[j], acc[j + 1]} * pdf2_t<MODE>(sc, isc, nm, f2{S[j], S[j + 1]}, mu);
         acc[j] = r.x;
         acc[j + 1] = r.y;
     }
+#else
+    // columns per wave-uniform test: 8 (Gaussian); 4 for the logistic
+    // densities, whose division keeps more values live (register budget)
+    constexpr int GM = MODE >= 2 && CBN_MULROW_GROUP > 4 ? 4 : CBN_MULROW_GROUP;
+    constexpr int G = NC < GM ? NC : GM;
+#pragma unroll
+    for (int g = 0; g < NC; g += G) {
+        float sv[G];  // this group's sample values: one scalar-load burst, one wait
+#pragma unroll
+        for (int j = 0; j < G; ++j) sv[j] = S[g + j];
+        f2 p[G / 2];
+        float lo = __builtin_inff();
+        bool bad = false;
+        pdf2_fast<G / 2, MODE>(sc, isc, nm, sv, mu, p, lo, bad);
+        if (__builtin_expect(__any(lo < -126.f || bad), 0)) {
+#pragma unroll
+            for (int j = 0; j < G; j += 2) p[j / 2] = pdf2_t<MODE>(sc, isc, nm, f2{sv[j], sv[j + 1]}, mu);
+        }
+#pragma unroll
+        for (int j = 0; j < G; j += 2) {
+            const f2 r = f2{acc[g + j], acc[g + j + 1]} * p[j / 2];
+            acc[g + j] = r.x;
+            acc[g + j + 1] = r.y;
+        }
+    }
+#endif
 }
 
 template <int NC, int MODE>
@@ -709,10 +828,14 @@ __device__ __forceinline__ void load_inputs_tab(const PEv& ev, int f, unsigned q
 // into the dynamic LDS), part 0 multiplies them in (part order) and writes.
 // Batches too small to give every SIMD several waves (131 072 queries of an
 // MLP: 2 048 waves for 1 024 SIMDs) run 2-4 parts.
+// Threads of a query-kernel block: 8 waves, or 6 when the factor split has
+// 3 or 6 parts (a block holds whole query groups of `parts` waves).
+inline int query_block_threads(int parts) { return parts % 3 == 0 ? 6 * kWave : kQThreads; }
+
 struct FSplit {
     int parts;
     int comb_off;
-    int f[5];
+    int f[7];
 };
 
 // Occupancy target per instantiation (waves per SIMD the register
@@ -721,7 +844,7 @@ struct FSplit {
 // weight / sample loads, the next factor's evidence) is only hidden with all
 // of them resident.
 #ifndef CBN_WPE_LIN
-#define CBN_WPE_LIN 8
+#define CBN_WPE_LIN 6  // round 5: 8 -> 6 (80 VGPRs: the column-pair groups of mul_row_t without spills)
 #endif
 #ifndef CBN_WPE_MLP
 #define CBN_WPE_MLP 1
@@ -753,7 +876,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         __syncthreads();
     }
     const int lane = threadIdx.x & (kWave - 1);
-    const int wpb = kQThreads / kWave;
+    const int wpb = blockDim.x / kWave;  // 8 waves; 6 for a 3- or 6-part split (query_block_threads)
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int tasks = QW * L;
     const int parts = sp.parts;
@@ -778,15 +901,31 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
         const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
-        if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qb, z);
-        else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
+        if constexpr (!(M1 && TAB)) {  // (the M1 table loop loads its own, two factors ahead)
+            if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qb, z);
+            else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
+        }
         if constexpr (M1 && TAB) {  // hot headers, one factor ahead
             const PHead* __restrict__ hd = reinterpret_cast<const PHead*>(img + cst_off + 4);
             PHead h = hd[fa < nf ? fa : nf - 1];
-            for (int f = fa; f < f1; ++f) {
-                float zn[kMaxP];
+            // Evidence two factors ahead in two buffers used in turn (round
+            // 5): no register copy at the end of a factor, and every input
+            // is loaded (an input that is not evidence reads the image's 0
+            // cell), so the compiler's waits count the loads -- the
+            // next factor's loads stay in flight while this one's are
+            // consumed.  (One buffer + a copy waited for vmcnt(0) every
+            // factor: the prefetch covered one factor's VALU, not a miss.)
+            const float* zcell = img + cst_off;  // {0, 1}: element 0 is 0
+            auto load_z = [&](int f, float (&zz)[kMaxP]) {
+                const int fi = f < f1 ? f : f1 - 1;  // (past the range: reload the last one, unused)
+                const PEv4 c = reinterpret_cast<const PEv4*>(ev.p)[fi > 0 ? fi : 0];
+#pragma unroll
+                for (int i = 0; i < kTabIn; ++i) zz[i] = gload_b(c.p[i] ? c.p[i] : zcell, c.p[i] ? qb : 0u);
+#pragma unroll
+                for (int i = kTabIn; i < kMaxP; ++i) zz[i] = 0.f;
+            };
+            auto eval = [&](int f, const float (&zz)[kMaxP]) {
                 const int fn = f + 1 < f1 ? f + 1 : f;
-                load_inputs_tab(ev, fn, qb, zn);
                 const PHead hn = hd[fn];
                 const float* R = img + h.row + col0;
                 if (h.kind != CBN_FACTOR_QUERY) {
@@ -795,20 +934,29 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 } else {
                     float mu;
                     if (HMAX == 0 || h.n_layers == 1) {
-                        mu = lin4(img + h.wp, z);
+                        mu = lin4(img + h.wp, zz);
                     } else {
                         const float* PW = img + h.wp;
                         switch (h.act) {
-                            case CBN_ACT_TANH: mu = mlp1p_nin<CBN_ACT_TANH, kTabIn>(PW, h.n_in, h.hid, z, CBN_ACT_TANH); break;
-                            case CBN_ACT_RELU: mu = mlp1p_nin<CBN_ACT_RELU, kTabIn>(PW, h.n_in, h.hid, z, CBN_ACT_RELU); break;
-                            default: mu = mlp1p_rt(PW, h.n_in, h.hid, z, h.act); break;
+                            case CBN_ACT_TANH: mu = mlp1p_nin<CBN_ACT_TANH, kTabIn>(PW, h.n_in, h.hid, zz, CBN_ACT_TANH); break;
+                            case CBN_ACT_RELU: mu = mlp1p_nin<CBN_ACT_RELU, kTabIn>(PW, h.n_in, h.hid, zz, CBN_ACT_RELU); break;
+                            default: mu = mlp1p_rt(PW, h.n_in, h.hid, zz, h.act); break;
                         }
                     }
                     mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, R, h.scale, h.inv_scale, h.norm, mu);
                 }
-#pragma unroll
-                for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
                 h = hn;
+            };
+            float zb[kMaxP];
+            load_z(fa, z);
+            load_z(fa + 1, zb);
+            for (int f = fa; f < f1; f += 2) {
+                eval(f, z);
+                load_z(f + 2, z);
+                if (f + 1 < f1) {
+                    eval(f + 1, zb);
+                    load_z(f + 3, zb);
+                }
             }
         } else
         for (int f = fa; f < f1; ++f) {
@@ -898,7 +1046,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
         max_out[blockIdx.x] = m;
     }
     if (blockIdx.x == 0)  // words of blocks this launch does not have
-        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += kQThreads) max_out[i] = 0u;
+        for (int i = (int)gridDim.x + threadIdx.x; i < n_words; i += blockDim.x) max_out[i] = 0u;
 }
 
 // Query-independent factors, once per plan: SHARED x[j] = mean_c pdf(s_j;
@@ -1323,7 +1471,7 @@ struct ParamPlan {
     size_t deep = 0; // dynamic LDS of the deep-model path (query kernel)
     size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
-    int split[3][5] = {};  // factor ranges for 1 / 2 / 4 parts (index parts >> 1)
+    int split[7][8] = {};  // factor ranges for 1, 2, 3, 4 and 6 parts (index: parts)
     float* d_image = nullptr;
     int* d_which = nullptr;
     int image_floats = 0;
@@ -1341,12 +1489,13 @@ void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long
     FSplit sp;
     memset(&sp, 0, sizeof(sp));
     sp.parts = parts;
-    for (int p = 0; p <= parts; ++p) sp.f[p] = pp->split[parts >> 1][p];
+    for (int p = 0; p <= parts; ++p) sp.f[p] = pp->split[parts][p];
     size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
     lds = (lds + 15) & ~(size_t)15;
     sp.comb_off = (int)(lds / sizeof(float));
     if (parts > 1) lds += (size_t)(kQThreads / kWave) * NC * kWave * sizeof(float);
-    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB, M1>), dim3(grid), dim3(kQThreads), lds, s, pp->d_image,
+    hipLaunchKernelGGL((k_param_query<NC, HMAX, MODE, TAB, M1>), dim3(grid), dim3(query_block_threads(parts)), lds, s,
+                       pp->d_image,
                        pp->cst_off, pp->nf, ev, Q, pp->N, L, QW, pp->max_slots, words, out, sp);
 }
 
@@ -1442,9 +1591,10 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
     int parts = pp->parts;
     if (const char* e = diag_env("CBN_PARAM_PARTS")) {
         const int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4) parts = v;
+        if (v == 1 || v == 2 || v == 3 || v == 4 || v == 6) parts = v;
     }
-    long long grid = (waves * parts + kQThreads / kWave - 1) / (kQThreads / kWave);
+    const int wpb = query_block_threads(parts) / kWave;
+    long long grid = (waves * parts + wpb - 1) / wpb;
     grid = std::max(1LL, std::min(grid, (long long)pp->max_slots));
     const bool raw = (flags & CBN_RUN_RAW) != 0;
     unsigned* words = raw ? max_bits : plan->d_sync + kMaxWordOff;
@@ -1711,6 +1861,10 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
     // Linear M1 plans with N >= 16 take 16-column chunks and four parts
     // (half the evidence loads and model evaluations of 8-column chunks at the
     // same 8 waves per SIMD): LR at 131 072 queries 54 -> 48 us, 1 M 377 -> 331 us.
+    // (Round 5: at 6 waves per SIMD, 4 parts make 1.33 rounds of waves; 3
+    // parts in 6-wave blocks -- one whole round at 131 072 queries --
+    // measured slower, 47.8-48.1 vs 43.3-43.6 us, 6 parts 52.2-52.5:
+    // profiles/r05_param_ab.json.  CBN_PARAM_PARTS=3|6 under CBN_DIAG.)
     pp->parts = n_factors >= 2 ? 2 : 1;
     pp->lin16 = pp->all_m1 && hmax == 0 && N >= 16;
     if (pp->all_m1 && (hmax == 1 || pp->lin16) && n_factors >= 8) pp->parts = 4;
@@ -1759,9 +1913,8 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             }
             total += cost[f];
         }
-        for (int k = 0; k < 3; ++k) {
-            const int parts = 1 << k;
-            int* b = pp->split[k];
+        for (int parts : {1, 2, 3, 4, 6}) {
+            int* b = pp->split[parts];
             b[0] = 0;
             int p = 1;
             double acc = 0;
