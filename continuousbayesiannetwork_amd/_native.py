@@ -170,6 +170,7 @@ CBN_E_TIMEOUT = -5
 CBN_PLAN_FAST, CBN_PLAN_LDS, CBN_PLAN_PAIRED, CBN_PLAN_STAGED = 1, 2, 4, 8
 CBN_PLAN_FUSED, CBN_PLAN_PARAMETRIC, CBN_PLAN_VPL2, CBN_PLAN_DIRECT = 16, 32, 64, 128
 CBN_PLAN_COLS = 256
+CBN_PLAN_SLOTS = 512
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

@@ -1376,6 +1376,240 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 }
 
 // ---------------------------------------------------------------------------
+// Slot-indexed kernel for global-table plans with >= 4 lanes per query (round
+// 5: the configs[4] grid, L = 8, 100 factors over 99 evidence slots).
+// k_query_fast loads each factor's parents' evidence itself: kFastObs = 4
+// loads per factor (absent parents included, so the waits count), 400 loads
+// per query for 99 distinct values, in two dependent chunks -- 15 us of a
+// ~40 us wave (stamps, profiles/r05_grid_zero_skip_ab.json).  Here, as in
+// k_query_cols, the L lanes of a query split its SLOTS: one load per slot,
+// all in flight, mapped to an int16 domain index in LDS; then each lane forms
+// the row offsets of factors l, l + L, ... from its parents' indices (ColRec:
+// base + sum(index x row weight), any index < 0 -> -1 = the zero row) into
+// the query's offset row in LDS -- once per factor, not once per lane as in
+// k_query_cols' product loop -- and the product loop is k_query_fast's
+// global-table loop (batches of row loads, LDS for the small tables in
+// lmask, the zero-product lane skip).  Same factor order, same products:
+// bit-identical to k_query_fast.  LDS: [small tables][QSlot ns][ColRec nf]
+// [slot pointers][sidx ns x QB][offsets QB x nf4][wave maxima]
+// (slots_lds_bytes, host).
+template <int VPL, int MODE>
+__global__ void __launch_bounds__(kQueryThreads)
+k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, const int* __restrict__ crec,
+              FPtrsT<kFastPtrsSmall> sp, long long Q, long long per, int N, int L, unsigned* __restrict__ sync,
+              unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
+              float* __restrict__ out, int lds_tab, unsigned long long lmask0, unsigned long long lmask1) {
+    CBN_STAMP_INIT;
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float* simg = reinterpret_cast<float*>(smem4);
+    const int tid = threadIdx.x;
+    constexpr int nthr = kQueryThreads;
+    const int lane = tid & (kWave - 1);
+    const int wid = tid / kWave;
+    const int QB = nthr / L;  // queries per block round
+    const int nf4 = (nf + 3) & ~3;
+    const QSlot* srec = reinterpret_cast<const QSlot*>(simg + lds_tab);
+    int* lcrec = reinterpret_cast<int*>(simg + lds_tab + ns * 4);
+    const float** sptr = reinterpret_cast<const float**>(lcrec + nf * kColRecInts);
+    short* sidx = reinterpret_cast<short*>(sptr + ((ns + 1) & ~1));
+    int* woff = reinterpret_cast<int*>(sidx + (((size_t)ns * QB + 7) & ~size_t(7)));
+    float* wmax = reinterpret_cast<float*>(woff + (size_t)QB * nf4);
+    const long long q0 = (long long)blockIdx.x * per;
+    const long long q1 = q0 + per < Q ? q0 + per : Q;
+    if (lds_tab > 0) lds_dma_copy(gimage, smem4, lds_tab / 4);            // the small tables
+    lds_dma_copy(gimage + qslot_off, smem4 + lds_tab / 4, ns);            // QSlot[ns] (16 B each)
+    for (int i = tid; i < nf * (kColRecInts / 4); i += nthr)
+        reinterpret_cast<int4*>(lcrec)[i] = reinterpret_cast<const int4*>(crec)[i];
+    if (tid < ns) sptr[tid] = sp.p[tid];
+    CBN_STAMP(1);
+    __syncthreads();
+    CBN_STAMP(2);
+    float maxv = 1.f;
+    if (MODE == kModeWrite) {
+        unsigned m = 0;
+        for (int i = lane; i < n_max; i += kWave) m = max(m, max_in[i]);
+        m = wave_max_u(m);
+        maxv = __uint_as_float(m);
+        if (max_out && blockIdx.x == 0 && tid == 0) *max_out = m;
+    }
+    float lmax = 0.f;
+    const int ql = tid / L;  // this lane's query within the block round
+    const int l = tid - ql * L;
+    const int nsl = (ns - l + L - 1) / L;  // slots this lane indexes: l, l + L, ...
+    int* my = woff + (size_t)ql * nf4;
+    int col[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) col[v] = (l * VPL + v) * 4;
+    constexpr int NV = 4 * VPL;
+    constexpr int CH = 16;  // slot loads in flight per lane (configs[4]: 13)
+    float acc[NV];
+    long long fq = -1;
+    bool first = true;
+    for (long long qb = q0; qb < q1; qb += QB) {  // block-uniform rounds
+        const long long qq = qb + ql;
+        const bool valid = qq < q1;
+        const long long q = valid ? qq : q0;
+        if (first) CBN_STAMP(3);
+        for (int c0 = 0; c0 < nsl; c0 += CH) {
+            float x[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                int s = l + (c0 + k) * L;
+                s = s < ns ? s : ns - 1;  // unconditional loads: the compiler's waits stay counted
+                x[k] = gload(sptr[s], q);
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const int s = l + (c0 + k) * L;
+                if (c0 + k < nsl) {
+                    const QSlot sr = srec[s];
+                    const float xv = x[k];
+                    int i;
+                    if (sr.dense) {
+                        i = (int)xv;
+                        i = (xv >= 0.f && xv < (float)sr.card && (float)i == xv) ? i : -1;
+                    } else {
+                        i = bsearch_eq(gimage + sr.dom_off, sr.card, xv);
+                    }
+                    sidx[s * QB + ql] = (short)i;
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the query's lanes are in this wave
+        __builtin_amdgcn_wave_barrier();
+        // row offsets of factors l, l + L, ... of this query
+        for (int f = l; f < nf; f += L) {
+            const int4 ra = reinterpret_cast<const int4*>(lcrec)[f * 2];
+            const int4 rb = reinterpret_cast<const int4*>(lcrec)[f * 2 + 1];
+            const int par[kFastObs] = {ra.z, ra.w, rb.x, rb.y};
+            int o = ra.x, neg = 0;
+#pragma unroll
+            for (int p = 0; p < kFastObs; ++p) {
+                if (p < ra.y) {
+                    const int iv = sidx[(par[p] >> 24) * QB + ql];
+                    neg |= iv;
+                    o += (int)__umul24((unsigned)iv, (unsigned)(par[p] & 0xFFFFFF));
+                }
+            }
+            my[f] = neg < 0 ? -1 : o;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (first) CBN_STAMP(4);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
+        // k_query_fast's global-table loop, zero-product lane skip included
+        constexpr int KB = VPL == 2 ? 6 : 8;
+        bool alive = true;
+        for (int f0 = 0; f0 < nf; f0 += KB) {
+            if (__builtin_amdgcn_ballot_w64(alive) == 0) break;
+            int oo[KB];
+#pragma unroll
+            for (int k = 0; k < KB; ++k) oo[k] = (f0 + k < nf && alive) ? my[f0 + k] : -1;
+            float4 t[KB][VPL];
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                const int o = oo[k];
+                const int fk = f0 + k;  // wave-uniform: is this factor's table in LDS?
+                const bool in_lds = fk < nf && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0);
+                if (in_lds) {
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v)
+                        t[k][v] = o >= 0 ? reinterpret_cast<const float4*>(simg + (o < 0 ? 0 : o))[l * VPL + v]
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                } else {
+                    const float4* row = reinterpret_cast<const float4*>(gimage + (o < 0 ? 0 : o)) + l * VPL;
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v)
+                        t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                if (f0 + k < nf) {
+#pragma unroll
+                    for (int v = 0; v < VPL; ++v) {
+                        acc[4 * v + 0] = acc[4 * v + 0] * t[k][v].x;
+                        acc[4 * v + 1] = acc[4 * v + 1] * t[k][v].y;
+                        acc[4 * v + 2] = acc[4 * v + 2] * t[k][v].z;
+                        acc[4 * v + 3] = acc[4 * v + 3] * t[k][v].w;
+                    }
+                }
+            }
+            bool nz = false;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) nz |= acc[i] != 0.f;  // (NaN counts as alive)
+            alive = nz;
+        }
+        if (first) CBN_STAMP(5);
+        if (valid) {
+            if (MODE == kModeFused) fq = q;
+            if (MODE == kModeWrite) {
+                float* o = out + q * N;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                        acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
+            } else if (MODE == kModeRaw) {
+                float* o = out + q * N;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v)
+                    *reinterpret_cast<float4*>(o + col[v]) =
+                        make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NV; ++i) lmax = fmaxf(lmax, acc[i]);
+            }
+        }
+        // the next round rewrites this query slot's indices and offsets (lanes of one wave)
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (first) CBN_STAMP(6);
+        first = false;
+    }
+    CBN_STAMP(7);
+    if (MODE == kModeMax || MODE == kModeRaw) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int i = 0; i < nthr / kWave; ++i) m = fmaxf(m, wmax[i]);
+            max_out[blockIdx.x] = __float_as_uint(m);
+        }
+        if (blockIdx.x == 0)
+            for (int i = (int)gridDim.x + tid; i < n_max; i += nthr) max_out[i] = 0u;
+    }
+    if (MODE == kModeFused) {
+        lmax = wave_max(lmax);
+        if (lane == 0) wmax[wid] = lmax;
+        __syncthreads();
+        if (wid == 0) {
+            const int nw = nthr / kWave;
+            const unsigned gm = slot_barrier_max(sync, epoch, wave_max(lane < nw ? wmax[lane] : 0.f));
+            if (lane == 0) {
+                wmax[0] = __uint_as_float(gm);
+                if (blockIdx.x == 0 && max_out) *max_out = gm;
+            }
+        }
+        CBN_STAMP(8);
+        __syncthreads();
+        CBN_STAMP(9);
+        maxv = wmax[0];
+        if (fq >= 0) {
+            float* o = out + fq * N;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v)
+                *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                    acc[4 * v] / maxv, acc[4 * v + 1] / maxv, acc[4 * v + 2] / maxv, acc[4 * v + 3] / maxv);
+        }
+        CBN_STAMP(10);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Staged fast kernel: the paired N = 32 layout in LDS (four lanes per query,
 // eight columns per lane, <= 32 factors), all four modes.  A block walks its
 // query range in rounds of kSR = 256 queries (16 waves x 16 queries).
@@ -1957,6 +2191,17 @@ FPtrsT<kFastPtrsSmall> slot_ptrs(const cbn_plan* p, const EvPtrs& ev) {
     return sp;
 }
 
+// dynamic LDS of k_query_slots (its layout, in order): the small tables,
+// QSlot[ns], ColRec[nf], slot pointers, sidx[ns][QB] (int16), offsets
+// [QB][nf4], wave maxima
+size_t slots_lds_bytes(long long lds_tab_floats, int ns, int nf, int QB) {
+    const size_t nf4 = (size_t)((nf + 3) & ~3);
+    size_t b = (size_t)lds_tab_floats * 4 + (size_t)ns * sizeof(QSlot) + (size_t)nf * sizeof(ColRec) +
+               (size_t)((ns + 1) & ~1) * sizeof(void*) + ((((size_t)ns * QB + 7) & ~size_t(7)) * 2) +
+               (size_t)QB * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
+    return (b + 15) & ~size_t(15);
+}
+
 // one fast-kernel launch with the pointer table sized to the plan
 template <int VPL, bool LDS, int MODE, int NP>
 void launch_fast_np(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPtrs& ev, long long Q, int L,
@@ -1985,6 +2230,13 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
                            fj, fast_ptrs<kFastPtrsSmall>(p, ev, p->prefix));
         return;
     }
+    if (p->slots) {
+        hipLaunchKernelGGL((k_query_slots<VPL, MODE>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s, p->nf,
+                           p->ns, p->d_image, p->rec_off + p->nf * kRecFloats, p->d_crec, slot_ptrs(p, ev), Q,
+                           (Q + blocks - 1) / blocks, p->N, L, p->d_sync, epoch, max_in, n_max, max_out, out,
+                           p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
+        return;
+    }
     if (p->cols) {
         auto k = (p->ns + L - 1) / L <= 16 ? k_query_cols<VPL, LDS, MODE, 16> : k_query_cols<VPL, LDS, MODE, 40>;
         hipLaunchKernelGGL(k, dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s,
@@ -2010,6 +2262,8 @@ const void* fast_kernel_fn(int nf, bool cols = false, int slots_per_lane = 0) {
 
 template <int VPL, bool LDS, int MODE>
 void allow_fast_lds(int bytes) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_slots<VPL, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrsSmall>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_query_fast<VPL, LDS, MODE, kFastPtrs>),
@@ -2309,9 +2563,19 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
         }
         if (vp > 0) {
             const long long nf4 = (n_factors + 3) & ~3;
-            const long long side = (long long)kFastPtrs * sizeof(void*) +
-                                   (long long)(kQueryThreads / kWave) * (kWave / Lp) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
-            const long long recb = (long long)n_factors * kRecFloats * 4;  // the records go to LDS too
+            long long side = (long long)kFastPtrs * sizeof(void*) +
+                             (long long)(kQueryThreads / kWave) * (kWave / Lp) * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
+            long long recb = (long long)n_factors * kRecFloats * 4;  // the records go to LDS too
+            if (Lp > 2 && !diag_env("CBN_NO_SLOTS")) {
+                // k_query_slots (>= 4 lanes per query) takes the plan if it can:
+                // budget the small tables beside ITS side buffers
+                int ns_est = 0;
+                for (int f = 0; f < n_factors; ++f)
+                    for (int q = 0; q < factors[f].n_parents && q < kMaxP; ++q)
+                        ns_est = std::max(ns_est, factors[f].parent_ev_slot[q] + 1);
+                side = (long long)slots_lds_bytes(0, ns_est, n_factors, kQueryThreads / Lp);
+                recb = 0;
+            }
             long long budget = (long long)kLdsBudget - side - recb - 1024;  // bytes
             if (2 * (side + recb) <= (long long)kLdsBudget)
                 budget = std::min(budget, (long long)kLdsBudget / 2 - side - recb - 1024);
@@ -2624,7 +2888,47 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                     P->fast_lds_bytes = cols_bytes;
                 }
             }
+            // slot-indexed kernel (k_query_slots, round 5): global-table plans of
+            // >= 4 lanes per query (the configs[4] grid) -- the slots' evidence
+            // loaded once per query instead of kFastObs loads per factor
+            if (!P->staged && !P->paired && !P->cols && !P->use_lds && Lf > 2 && ns <= kFastPtrsSmall &&
+                n_factors <= 128 && !diag_env("CBN_NO_SLOTS")) {
+                bool ok_s = true;
+                for (int sl = 0; sl < ns; ++sl) ok_s = ok_s && slot_card[sl] <= 32767;
+                for (int f = 0; f < n_factors && ok_s; ++f)
+                    for (int q = 0; q < recs[f].n_obs; ++q)
+                        ok_s = ok_s && (recs[f].card[q] & (kDenseBit - 1)) == slot_card[recs[f].slot[q]];
+                std::vector<ColRec> cr(n_factors);
+                for (int f = 0; f < n_factors && ok_s; ++f) {
+                    ColRec& c = cr[f];
+                    memset(&c, 0, sizeof(c));
+                    c.base = recs[f].table_off;
+                    c.n_obs = recs[f].n_obs;
+                    c.lds = ((lds_mask[f >> 6] >> (f & 63)) & 1ull) ? 1 : 0;
+                    long long w = RS;
+                    for (int q = recs[f].n_obs - 1; q >= 0; --q) {
+                        ok_s = ok_s && w < (1LL << 24) && recs[f].slot[q] < 256;
+                        c.par[q] = (recs[f].slot[q] << 24) | (int)(w & 0xFFFFFF);
+                        w *= recs[f].card[q] & (kDenseBit - 1);
+                    }
+                    // the offset (table base + row x RS) must fit an int
+                    ok_s = ok_s && (long long)recs[f].table_off + w < (1LL << 31);
+                }
+                const size_t sb = slots_lds_bytes(P->lds_tab_floats, ns, n_factors, kQueryThreads / Lf);
+                if (ok_s && sb <= (size_t)kLdsBudget) {
+                    if (hipMalloc(&P->d_crec, sizeof(ColRec) * n_factors) != hipSuccess ||
+                        hipMemcpy(P->d_crec, cr.data(), sizeof(ColRec) * n_factors, hipMemcpyHostToDevice) !=
+                            hipSuccess) {
+                        cbn_plan_destroy(P);
+                        return set_err(CBN_E_HIP, "cbn_plan_create: slot records upload failed");
+                    }
+                    P->slots = true;
+                    P->fast_lds_bytes = sb;
+                }
+            }
             P->fast_blocks_per_cu = 2 * P->fast_lds_bytes <= (size_t)kLdsBudget ? 2 : 1;
+            if (P->slots)
+                if (const char* e = diag_env("CBN_SLOTS_BPC")) P->fast_blocks_per_cu = atoi(e) == 2 ? 2 : 1;
             P->max_slots = std::min(num_cu() * P->fast_blocks_per_cu, kMaxSlots);
             if (hipMemcpy(P->d_image + rec_off, recs.data(), sizeof(FastRec) * n_factors, hipMemcpyHostToDevice) !=
                     hipSuccess ||
@@ -2643,6 +2947,8 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
                 int nb = 0;
                 const int spl = (ns + Lf - 1) / Lf;  // k_query_cols: slots per lane
                 const void* fn = P->staged ? reinterpret_cast<const void*>(&k_query_staged<kModeFused>)
+                                 : P->slots ? (vpl == 2 ? reinterpret_cast<const void*>(&k_query_slots<2, kModeFused>)
+                                                        : reinterpret_cast<const void*>(&k_query_slots<1, kModeFused>))
                                  : P->use_lds ? (vpl == 2 ? fast_kernel_fn<2, true, kModeFused>(n_factors, P->cols, spl)
                                                           : fast_kernel_fn<1, true, kModeFused>(n_factors, P->cols, spl))
                                               : (vpl == 2 ? fast_kernel_fn<2, false, kModeFused>(n_factors, P->cols, spl)
@@ -2968,7 +3274,7 @@ int32_t cbn_plan_flags(const cbn_plan* plan) {
            (plan->paired ? CBN_PLAN_PAIRED : 0) | (plan->staged ? CBN_PLAN_STAGED : 0) |
            (plan->fused_ok ? CBN_PLAN_FUSED : 0) | (plan->param ? CBN_PLAN_PARAMETRIC : 0) |
            (plan->vpl == 2 ? CBN_PLAN_VPL2 : 0) | (plan->direct ? CBN_PLAN_DIRECT : 0) |
-           (plan->cols ? CBN_PLAN_COLS : 0);
+           (plan->cols ? CBN_PLAN_COLS : 0) | (plan->slots ? CBN_PLAN_SLOTS : 0);
 }
 
 int32_t cbn_plan_max_words(const cbn_plan* plan) {

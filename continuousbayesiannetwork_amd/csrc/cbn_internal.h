@@ -89,6 +89,7 @@ struct cbn_plan {
     bool staged = false;         // paired plans of <= 32 factors: k_query_staged (evidence staged by factor)
     size_t staged_lds_bytes = 0;
     bool cols = false;           // non-paired fast plans: k_query_cols (evidence indexed per slot, round 4)
+    bool slots = false;          // global-table plans of >= 4 lanes per query: k_query_slots (round 5)
     int zero_off = -1;
     int prefix = 0;              // staged plans: leading 1-row factors folded into factor `prefix` (k_merge_prefix)
     int prefix_offs[9] = {};     // table offsets of factors 0..prefix

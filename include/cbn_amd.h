@@ -246,6 +246,7 @@ int cbn_plan_check(cbn_plan* plan);
 #define CBN_PLAN_VPL2 64       /* 8 output columns per lane */
 #define CBN_PLAN_DIRECT 128    /* direct plan (cbn_plan_create_direct) */
 #define CBN_PLAN_COLS 256      /* k_query_cols (evidence indexed once per slot; non-paired table plans) */
+#define CBN_PLAN_SLOTS 512     /* k_query_slots (slot-indexed evidence, global tables, >= 4 lanes per query; round 5) */
 int32_t cbn_plan_flags(const cbn_plan* plan);
 
 /* Test hook: mark the plan as if a single-launch call had timed out in its
