@@ -1498,20 +1498,24 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
         if (first) CBN_STAMP(4);
 #pragma unroll
         for (int i = 0; i < NV; ++i) acc[i] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
-        // k_query_fast's global-table loop, zero-product lane skip included
+        // Phase A: the first FA factors for every lane -- k_query_fast's
+        // global-table loop with the zero-product lane skip.  On a peaked
+        // network most lanes are all-zero by then (configs[4]: 87 % of the
+        // lanes by factor 12, profiles/r05_zero_histogram.json).
         constexpr int KB = VPL == 2 ? 6 : 8;
+        const int FA = nf < 2 * KB ? nf : 2 * KB;
         bool alive = true;
-        for (int f0 = 0; f0 < nf; f0 += KB) {
+        for (int f0 = 0; f0 < FA; f0 += KB) {
             if (__builtin_amdgcn_ballot_w64(alive) == 0) break;
             int oo[KB];
 #pragma unroll
-            for (int k = 0; k < KB; ++k) oo[k] = (f0 + k < nf && alive) ? my[f0 + k] : -1;
+            for (int k = 0; k < KB; ++k) oo[k] = (f0 + k < FA && alive) ? my[f0 + k] : -1;
             float4 t[KB][VPL];
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
                 const int o = oo[k];
                 const int fk = f0 + k;  // wave-uniform: is this factor's table in LDS?
-                const bool in_lds = fk < nf && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0);
+                const bool in_lds = fk < FA && (((fk < 64 ? lmask0 >> fk : lmask1 >> (fk - 64)) & 1ull) != 0);
                 if (in_lds) {
 #pragma unroll
                     for (int v = 0; v < VPL; ++v)
@@ -1521,12 +1525,12 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
                     const float4* row = reinterpret_cast<const float4*>(gimage + (o < 0 ? 0 : o)) + l * VPL;
 #pragma unroll
                     for (int v = 0; v < VPL; ++v)
-                        t[k][v] = (fk < nf && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        t[k][v] = (fk < FA && o >= 0) ? row[v] : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
-                if (f0 + k < nf) {
+                if (f0 + k < FA) {
 #pragma unroll
                     for (int v = 0; v < VPL; ++v) {
                         acc[4 * v + 0] = acc[4 * v + 0] * t[k][v].x;
@@ -1540,6 +1544,90 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
 #pragma unroll
             for (int i = 0; i < NV; ++i) nz |= acc[i] != 0.f;  // (NaN counts as alive)
             alive = nz;
+        }
+        // Phase B: the surviving lanes, up to 8 per pass, one per 8-lane group.
+        // A lane's remaining factors are a dependent chain of row loads that
+        // the survivors alone would walk 6 rows at a time (a wave waits one
+        // load latency per batch however few lanes live); here the group's 8
+        // lanes load the rows of 8 x R consecutive factors of ONE survivor at
+        // once (its query's offsets, its column block), and the running
+        // product then visits lane 0, 1, ..., 7 of the group -- each
+        // multiplying its R rows in factor order -- so every survivor's
+        // product is the same sequence of fp32 multiplies as in phase A's
+        // loop: the same bits, one load latency per 8 x R factors.
+        if (FA < nf) {
+            constexpr int R = 4;  // rows per lane per chunk: a chunk is 32 factors
+            unsigned long long am = __builtin_amdgcn_ballot_w64(alive);
+            const int gq = lane >> 3, j = lane & 7;
+            while (am) {  // wave-uniform
+                unsigned long long pass = 0, m = am;
+                int src = -1;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (m) {
+                        const int b = __builtin_ctzll(m);
+                        if (gq == k) src = b;
+                        pass |= 1ull << b;
+                        m &= m - 1;
+                    }
+                }
+                am = m;
+                const int sl = src < 0 ? lane : src;  // the group's survivor lane (idle group: its own, unused)
+                float cur[NV];
+#pragma unroll
+                for (int i = 0; i < NV; ++i) cur[i] = __shfl(acc[i], sl, kWave);
+                const int* qoff = woff + (size_t)((wid * kWave + sl) / L) * nf4;
+                const int il = sl & (L - 1);  // the survivor's column block
+                for (int c0 = FA; c0 < nf; c0 += 8 * R) {
+                    float4 t[R][VPL];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int f = c0 + j * R + r;
+                        const int o = (src >= 0 && f < nf) ? qoff[f] : -1;
+                        const bool in_lds = f < nf && (((f < 64 ? lmask0 >> f : lmask1 >> (f - 64)) & 1ull) != 0);
+#pragma unroll
+                        for (int v = 0; v < VPL; ++v) t[r][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (o >= 0) {
+                            if (in_lds) {
+#pragma unroll
+                                for (int v = 0; v < VPL; ++v)
+                                    t[r][v] = reinterpret_cast<const float4*>(simg + o)[il * VPL + v];
+                            } else {
+#pragma unroll
+                                for (int v = 0; v < VPL; ++v)
+                                    t[r][v] = reinterpret_cast<const float4*>(gimage + o)[il * VPL + v];
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < 8; ++s2) {
+                        if (j == s2) {
+#pragma unroll
+                            for (int r = 0; r < R; ++r) {
+                                if (c0 + s2 * R + r < nf) {
+#pragma unroll
+                                    for (int v = 0; v < VPL; ++v) {
+                                        cur[4 * v + 0] = cur[4 * v + 0] * t[r][v].x;
+                                        cur[4 * v + 1] = cur[4 * v + 1] * t[r][v].y;
+                                        cur[4 * v + 2] = cur[4 * v + 2] * t[r][v].z;
+                                        cur[4 * v + 3] = cur[4 * v + 3] * t[r][v].w;
+                                    }
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < NV; ++i) cur[i] = __shfl(cur[i], (lane & ~7) | s2, kWave);
+                    }
+                }
+                // back to the survivor's own lane (taken by group popcount(pass below it))
+                const bool mine = ((pass >> lane) & 1ull) != 0;
+                const int back = mine ? 8 * __builtin_popcountll(pass & ((1ull << lane) - 1ull)) : lane;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) {
+                    const float v = __shfl(cur[i], back, kWave);
+                    if (mine) acc[i] = v;
+                }
+            }
         }
         if (first) CBN_STAMP(5);
         if (valid) {
