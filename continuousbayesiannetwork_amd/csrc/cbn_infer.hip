@@ -1393,6 +1393,12 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // bit-identical to k_query_fast.  LDS: [small tables][QSlot ns][ColRec nf]
 // [slot pointers][sidx ns x QB][offsets QB x nf4][wave maxima]
 // (slots_lds_bytes, host).
+#ifndef CBN_SLOTS_FA
+#define CBN_SLOTS_FA 2  // phase A: batches of KB factors for every lane
+#endif
+#ifndef CBN_SLOTS_R
+#define CBN_SLOTS_R 4  // phase B: rows per lane per chunk
+#endif
 template <int VPL, int MODE>
 __global__ void __launch_bounds__(kQueryThreads)
 k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, const int* __restrict__ crec,
@@ -1503,7 +1509,7 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
         // network most lanes are all-zero by then (configs[4]: 87 % of the
         // lanes by factor 12, profiles/r05_zero_histogram.json).
         constexpr int KB = VPL == 2 ? 6 : 8;
-        const int FA = nf < 2 * KB ? nf : 2 * KB;
+        const int FA = nf < CBN_SLOTS_FA * KB ? nf : CBN_SLOTS_FA * KB;
         bool alive = true;
         for (int f0 = 0; f0 < FA; f0 += KB) {
             if (__builtin_amdgcn_ballot_w64(alive) == 0) break;
@@ -1556,7 +1562,7 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
         // product is the same sequence of fp32 multiplies as in phase A's
         // loop: the same bits, one load latency per 8 x R factors.
         if (FA < nf) {
-            constexpr int R = 4;  // rows per lane per chunk: a chunk is 32 factors
+            constexpr int R = CBN_SLOTS_R;  // rows per lane per chunk: a chunk is 8 R factors
             unsigned long long am = __builtin_amdgcn_ballot_w64(alive);
             const int gq = lane >> 3, j = lane & 7;
             while (am) {  // wave-uniform
