@@ -1391,8 +1391,20 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 // global-table loop (batches of row loads, LDS for the small tables in
 // lmask, the zero-product lane skip).  Same factor order, same products:
 // bit-identical to k_query_fast.  LDS: [small tables][QSlot ns][ColRec nf]
-// [slot pointers][sidx ns x QB][offsets QB x nf4][wave maxima]
+// [slot pointers][sidx ns x SQ][offsets QB x nf4][wave maxima]
 // (slots_lds_bytes, host).
+// sidx row stride (int16 units) of k_query_slots: QB plus a pad of 16 / L
+// dwords (>= 1).  An unpadded [ns][QB] layout puts every lane of a query pair
+// on one bank (QB / 2 dwords is a multiple of 32), so the index writes and the
+// offset phase's parent reads were 8-way conflicts; with the pad a slot row
+// shifts the bank by 16 / L, and the 32 / L query pairs of a 32-lane group x
+// L consecutive slots land on distinct banks.
+__host__ __device__ __forceinline__ int slots_sidx_stride(int L) {
+    return kQueryThreads / L + 2 * (L >= 16 ? 1 : 16 / L);
+}
+#ifndef CBN_SLOTS_DPP
+#define CBN_SLOTS_DPP 1  // phase B hands the running product on by DPP row shifts (0: ds_bpermute)
+#endif
 #ifndef CBN_SLOTS_FA
 #define CBN_SLOTS_FA 2  // phase A: batches of KB factors for every lane
 #endif
@@ -1418,7 +1430,8 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
     int* lcrec = reinterpret_cast<int*>(simg + lds_tab + ns * 4);
     const float** sptr = reinterpret_cast<const float**>(lcrec + nf * kColRecInts);
     short* sidx = reinterpret_cast<short*>(sptr + ((ns + 1) & ~1));
-    int* woff = reinterpret_cast<int*>(sidx + (((size_t)ns * QB + 7) & ~size_t(7)));
+    const int SQ = slots_sidx_stride(L);
+    int* woff = reinterpret_cast<int*>(sidx + (((size_t)ns * SQ + 7) & ~size_t(7)));
     float* wmax = reinterpret_cast<float*>(woff + (size_t)QB * nf4);
     const long long q0 = (long long)blockIdx.x * per;
     const long long q1 = q0 + per < Q ? q0 + per : Q;
@@ -1477,7 +1490,7 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
                     } else {
                         i = bsearch_eq(gimage + sr.dom_off, sr.card, xv);
                     }
-                    sidx[s * QB + ql] = (short)i;
+                    sidx[s * SQ + ql] = (short)i;
                 }
             }
         }
@@ -1492,7 +1505,7 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
 #pragma unroll
             for (int p = 0; p < kFastObs; ++p) {
                 if (p < ra.y) {
-                    const int iv = sidx[(par[p] >> 24) * QB + ql];
+                    const int iv = sidx[(par[p] >> 24) * SQ + ql];
                     neg |= iv;
                     o += (int)__umul24((unsigned)iv, (unsigned)(par[p] & 0xFFFFFF));
                 }
@@ -1621,8 +1634,19 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
                                 }
                             }
                         }
+                        if (CBN_SLOTS_DPP && s2 < 7) {
+                            // to the next lane only: a DPP row shift (a VALU move, no
+                            // LDS round trip); lanes other than s2 + 1 take values
+                            // they overwrite before their own turn
 #pragma unroll
-                        for (int i = 0; i < NV; ++i) cur[i] = __shfl(cur[i], (lane & ~7) | s2, kWave);
+                            for (int i = 0; i < NV; ++i)
+                                cur[i] = __int_as_float(__builtin_amdgcn_update_dpp(
+                                    __float_as_int(cur[i]), __float_as_int(cur[i]), 0x111 /* row_shr:1 */, 0xF, 0xF,
+                                    false));
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < NV; ++i) cur[i] = __shfl(cur[i], (lane & ~7) | s2, kWave);
+                        }
                     }
                 }
                 // back to the survivor's own lane (taken by group popcount(pass below it))
@@ -2286,12 +2310,13 @@ FPtrsT<kFastPtrsSmall> slot_ptrs(const cbn_plan* p, const EvPtrs& ev) {
 }
 
 // dynamic LDS of k_query_slots (its layout, in order): the small tables,
-// QSlot[ns], ColRec[nf], slot pointers, sidx[ns][QB] (int16), offsets
-// [QB][nf4], wave maxima
+// QSlot[ns], ColRec[nf], slot pointers, sidx[ns][SQ] (int16, SQ = QB + pad),
+// offsets [QB][nf4], wave maxima
 size_t slots_lds_bytes(long long lds_tab_floats, int ns, int nf, int QB) {
     const size_t nf4 = (size_t)((nf + 3) & ~3);
+    const size_t SQ = (size_t)slots_sidx_stride(kQueryThreads / QB);
     size_t b = (size_t)lds_tab_floats * 4 + (size_t)ns * sizeof(QSlot) + (size_t)nf * sizeof(ColRec) +
-               (size_t)((ns + 1) & ~1) * sizeof(void*) + ((((size_t)ns * QB + 7) & ~size_t(7)) * 2) +
+               (size_t)((ns + 1) & ~1) * sizeof(void*) + ((((size_t)ns * SQ + 7) & ~size_t(7)) * 2) +
                (size_t)QB * nf4 * 4 + (kQueryThreads / kWave) * 4 + 64;
     return (b + 15) & ~size_t(15);
 }

@@ -7,7 +7,7 @@ for d in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
         if "k_query" in r["Kernel_Name"]:
-            k = r["Kernel_Name"].split("(")[0].replace("void (anonymous namespace)::", "")
+            k = r["Kernel_Name"].replace("void (anonymous namespace)::", "").split("(")[0]
             agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
         print(d, k, {c: round(sum(x) / len(x)) for c, x in v.items()})
