@@ -622,6 +622,44 @@ def test_grid_fast_path_beyond_64_factors(gpu):
     np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), a.cpu().numpy())
 
 
+@pytest.mark.parametrize("d,side,Q", [(32, 5, 70001), (64, 4, 40001), (128, 4, 20001)])
+def test_slots_plan_lane_counts_rounds_and_survivors(d, side, Q, gpu):
+    """k_query_slots (CBN_PLAN_SLOTS: global-table plans of >= 4 lanes per
+    query) at L = 4, 8 and 16 lanes per query (N = 32, 64, 128), with more
+    queries than one block round holds (ragged last round), a peaked grid whose
+    products leave survivors for the phase-B chain, and off-domain evidence
+    (the zero row) on a few queries: fused == two launches bit for bit; a
+    sample of rows plus the batch argmax row matches the oracle on that
+    sample (same normaliser) at rtol 1e-5."""
+    from continuousbayesiannetwork_amd import _native
+
+    from helpers import grid_data
+
+    data, cols, edges = grid_data(100000, 7, side=side, d=d, keep=0.995, noise=0)
+    target, names = cols[-1], cols[:-1]
+    ev = sample_evidence(data, cols, names, Q, 3)
+    ev[names[3]][5:9] = float(d + 7)  # off-domain: those queries' rows are all zero
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    evt = _t(ev, gpu)
+    random.seed(4)
+    pdf, _ = bn.infer(target, evt, N_max=d)
+    fp = bn.engine._fast[(target, tuple(ev.keys()), d)]
+    assert _native.load().cbn_plan_flags(fp.plan.handle) & _native.CBN_PLAN_SLOTS
+    p = pdf.cpu().numpy()
+    assert p.max() == 1.0 and (p[5:9] == 0).all()
+    assert 0.05 < (p > 0).any(1).mean() < 1.0  # survivors and dead queries both present
+    bn.engine.fused = not bn.engine.fused
+    random.seed(4)
+    p2, _ = bn.infer(target, evt, N_max=d)
+    np.testing.assert_array_equal(p2.cpu().numpy(), p)
+    rstar = int(np.argmax(p.max(1)))
+    sub = np.append(np.append(np.arange(0, Q, Q // 40)[:40], [5, Q - 1]), rstar)
+    random.seed(4)
+    ref, _ = OracleBN(edges, cols, data).infer(target, {k: v[sub] for k, v in ev.items()}, d)
+    assert ref[-1].max() == 1.0
+    np.testing.assert_allclose(p[sub], ref, rtol=RTOL, atol=ATOL)
+
+
 def test_redrawn_domains_reuse_one_plan(gpu):
     """N_max above a domain's size: the reference pads it with new random
     values on every call (node.py:302-333).  The engine keeps ONE plan per
