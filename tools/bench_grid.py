@@ -77,9 +77,14 @@ def run(keep, noise, prof=False):
         g_tbs = gather / t / 1e12
         r = dict(label="headline (finite products)" if keep > 0.9 else
                  "DEGENERATE: every product underflows, all marginals NaN (as the reference)",
-                 roofline=dict(bound="L2/MALL row gather", achieved_TBps=round(g_tbs, 2),
+                 roofline=dict(bound="L2/MALL row gather", nominal_TBps=round(g_tbs, 2),
                                peak_l2_shared_rows_TBps=16.8, peak_mall_random_rows_TBps=8.6,
-                               frac_of_l2_peak=round(g_tbs / 16.8, 3), gather_bytes_per_call=gather),
+                               nominal_frac_of_l2_peak=round(g_tbs / 16.8, 3), nominal_gather_bytes_per_call=gather,
+                               note="nominal = every query gathers every factor's row; the table kernels skip "
+                                    "the rows of lanes whose products are already all +0 (round 5), so on the "
+                                    "peaked network the nominal rate exceeds the L2 figure: PMC counts 6.46 M "
+                                    "128-B TCP->TCC reads (0.83 GB) per 65 536-query call "
+                                    "(profiles/r05_grid_pmc.json)"),
                  queries=Q, factors=len(plan.factors), us_per_call=round(t * 1e6, 1), queries_per_s=round(Q / t, 1),
                  effective_GBps=round(byt / t / 1e9, 1), image_MB=round(lib.cbn_plan_table_bytes(plan.handle) / 1e6, 1)
                  if lib else None, fast_path=bool(lib.cbn_plan_max_words(plan.handle)) if lib else None,
