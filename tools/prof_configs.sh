@@ -1,0 +1,18 @@
+#!/bin/bash
+# rocprofv3 --kernel-trace --stats of the secondary configs' bench scripts
+# (configs[2] alarm, configs[3] cont, configs[4] grid --profile), one run each;
+# the kernel_stats CSVs land in gpurun_out/$OUT/<name>/
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/${OUT:-prof_configs}; mkdir -p $O; export TMPDIR=/tmp
+for b in alarm cont "grid --profile"; do
+  n=${b%% *}
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/$n -o run --output-format csv -- python3 tools/bench_$b.py > $O/$n.log 2>&1 || exit $?
+  rm -f $O/$n/run_kernel_trace.csv
+  python3 - "$O/$n/run_kernel_stats.csv" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "k_" in r["Name"]:
+        print(r["Name"].split("(")[0][:70], r["Calls"], round(float(r["AverageNs"]) / 1000, 2), "us avg")
+PY
+done
