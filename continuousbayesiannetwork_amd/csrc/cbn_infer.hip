@@ -1402,6 +1402,9 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
 __host__ __device__ __forceinline__ int slots_sidx_stride(int L) {
     return kQueryThreads / L + 2 * (L >= 16 ? 1 : 16 / L);
 }
+#ifndef CBN_SLOTS_FUSED2
+#define CBN_SLOTS_FUSED2 1  // fused single launch up to two block rounds (0: one round, beyond -> raw + scale)
+#endif
 #ifndef CBN_SLOTS_DPP
 #define CBN_SLOTS_DPP 1  // phase B hands the running product on by DPP row shifts (0: ds_bpermute)
 #endif
@@ -1463,6 +1466,12 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
     constexpr int CH = 16;  // slot loads in flight per lane (configs[4]: 13)
     float acc[NV];
     long long fq = -1;
+    // fused: up to two rounds per block (round 5) -- round 0's products wait in
+    // acc0 (query fq0) for the grid barrier beside round 1's in acc (query fq)
+    long long fq0 = -1;
+    float acc0[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) acc0[i] = 0.f;
     bool first = true;
     for (long long qb = q0; qb < q1; qb += QB) {  // block-uniform rounds
         const long long qq = qb + ql;
@@ -1660,8 +1669,13 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
             }
         }
         if (first) CBN_STAMP(5);
+        if (MODE == kModeFused && first) {  // (block-uniform) round 0: held until the barrier
+            fq0 = valid ? q : -1;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc0[i] = acc[i];
+        }
         if (valid) {
-            if (MODE == kModeFused) fq = q;
+            if (MODE == kModeFused && !first) fq = q;
             if (MODE == kModeWrite) {
                 float* o = out + q * N;
 #pragma unroll
@@ -1716,6 +1730,13 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
         __syncthreads();
         CBN_STAMP(9);
         maxv = wmax[0];
+        if (fq0 >= 0) {
+            float* o = out + fq0 * N;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v)
+                *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                    acc0[4 * v] / maxv, acc0[4 * v + 1] / maxv, acc0[4 * v + 2] / maxv, acc0[4 * v + 3] / maxv);
+        }
         if (fq >= 0) {
             float* o = out + fq * N;
 #pragma unroll
@@ -2415,7 +2436,10 @@ template <int VPL, bool LDS>
 int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bits, float* out, hipStream_t s) {
     const int L = p->N / (4 * VPL);
     const long long per_block = (long long)(kQueryThreads / kWave) * (kWave / L);
-    const long long blocks = (Q + per_block - 1) / per_block;
+    long long blocks = (Q + per_block - 1) / per_block;
+    // k_query_slots: beyond one round per block, every CU's block takes two
+    // (fused_capacity allows Q <= 2 rounds of the co-resident grid)
+    if (p->slots && CBN_SLOTS_FUSED2) blocks = std::min<long long>(blocks, std::min<long long>(num_cu(), kMaxSlots));
     const unsigned epoch = ++p->fused_epoch;  // 1, 2, ... (0 = never published)
     if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
     launch_fast_k<VPL, LDS, kModeFused>(p, (unsigned)blocks, s, ev, Q, L, epoch, nullptr, 0, max_bits, out);
@@ -2519,7 +2543,8 @@ long long fused_capacity(const cbn_plan* p) {
     if (!p->fast || !p->fused_ok) return 0;
     const int L = p->N / (4 * p->vpl);
     const long long blocks = std::min(num_cu(), kMaxSlots);  // one block per CU, one barrier slot each
-    return blocks * (kQueryThreads / kWave) * (kWave / L);
+    // k_query_slots holds two rounds of products per lane across the barrier
+    return blocks * (kQueryThreads / kWave) * (kWave / L) * (p->slots && CBN_SLOTS_FUSED2 ? 2 : 1);
 }
 
 }  // namespace
