@@ -1201,6 +1201,12 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
     constexpr int NV = 4 * VPL;
     float acc[NV];
     long long fq = -1;
+    // fused: up to two rounds per block (as k_query_slots): round 0's products
+    // wait in acc0 (query fq0) for the grid barrier
+    long long fq0 = -1;
+    float acc0[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) acc0[i] = 0.f;
     bool first = true;
     for (long long qb = q0; qb < q1; qb += QB) {  // block-uniform rounds
         const long long qq = qb + ql;
@@ -1308,8 +1314,13 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
             }
         }
         if (first) CBN_STAMP(5);
+        if (MODE == kModeFused && first) {  // (block-uniform) round 0: held until the barrier
+            fq0 = valid ? q : -1;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc0[i] = acc[i];
+        }
         if (valid) {
-            if (MODE == kModeFused) fq = q;
+            if (MODE == kModeFused && !first) fq = q;
             if (MODE == kModeWrite) {
                 float* o = out + q * N;
 #pragma unroll
@@ -1364,6 +1375,13 @@ k_query_cols(int rec_off, int nf, int ns, const float* __restrict__ gimage, int 
         __syncthreads();
         CBN_STAMP(9);
         maxv = wmax[0];
+        if (fq0 >= 0) {
+            float* o = out + fq0 * N;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v)
+                *reinterpret_cast<float4*>(o + col[v]) = make_float4(
+                    acc0[4 * v] / maxv, acc0[4 * v + 1] / maxv, acc0[4 * v + 2] / maxv, acc0[4 * v + 3] / maxv);
+        }
         if (fq >= 0) {
             float* o = out + fq * N;
 #pragma unroll
@@ -2437,9 +2455,9 @@ int launch_fused_v(cbn_plan* p, long long Q, const EvPtrs& ev, unsigned* max_bit
     const int L = p->N / (4 * VPL);
     const long long per_block = (long long)(kQueryThreads / kWave) * (kWave / L);
     long long blocks = (Q + per_block - 1) / per_block;
-    // k_query_slots: beyond one round per block, every CU's block takes two
+    // k_query_slots / k_query_cols: beyond one round per block, every CU's block takes two
     // (fused_capacity allows Q <= 2 rounds of the co-resident grid)
-    if (p->slots && CBN_SLOTS_FUSED2) blocks = std::min<long long>(blocks, std::min<long long>(num_cu(), kMaxSlots));
+    if ((p->slots || p->cols) && CBN_SLOTS_FUSED2) blocks = std::min<long long>(blocks, std::min<long long>(num_cu(), kMaxSlots));
     const unsigned epoch = ++p->fused_epoch;  // 1, 2, ... (0 = never published)
     if (p->fused_epoch == 0xFFFFFFFFu) p->fused_epoch = 0;
     launch_fast_k<VPL, LDS, kModeFused>(p, (unsigned)blocks, s, ev, Q, L, epoch, nullptr, 0, max_bits, out);
@@ -2543,8 +2561,8 @@ long long fused_capacity(const cbn_plan* p) {
     if (!p->fast || !p->fused_ok) return 0;
     const int L = p->N / (4 * p->vpl);
     const long long blocks = std::min(num_cu(), kMaxSlots);  // one block per CU, one barrier slot each
-    // k_query_slots holds two rounds of products per lane across the barrier
-    return blocks * (kQueryThreads / kWave) * (kWave / L) * (p->slots && CBN_SLOTS_FUSED2 ? 2 : 1);
+    // k_query_slots and k_query_cols hold two rounds of products per lane across the barrier
+    return blocks * (kQueryThreads / kWave) * (kWave / L) * ((p->slots || p->cols) && CBN_SLOTS_FUSED2 ? 2 : 1);
 }
 
 }  // namespace

@@ -622,6 +622,43 @@ def test_grid_fast_path_beyond_64_factors(gpu):
     np.testing.assert_array_equal(torch.cat(rows).cpu().numpy(), a.cpu().numpy())
 
 
+@pytest.mark.parametrize("which,Q", [("chain16", 200001), ("alarm", 300001)])
+def test_cols_plan_fused_two_rounds(which, Q, gpu):
+    """k_query_cols' fused single launch over two block rounds (round 5: the
+    first round's products held in registers across the grid barrier) == the
+    two-launch path bit for bit, with more queries than one round of the
+    co-resident grid holds (N = 16 chain: 2 lanes per query; the configs[2]
+    alarm plan: 1 lane per query); a sample plus the argmax row matches the
+    oracle on that sample (same normaliser)."""
+    from continuousbayesiannetwork_amd import _native
+
+    if which == "chain16":
+        data, cols, edges = chain_data(20, 16, 60000, 8, stay=0.8)
+        target, N = "X19", 16
+    else:
+        data, cols, edges = alarm_like_data(50000, 5)
+        target, N = "X35", 8
+    names = [c for c in cols if c != target]
+    ev = sample_evidence(data, cols, names, Q, 12)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    evt = _t(ev, gpu)
+    pdf, _ = bn.infer(target, evt, N_max=N)
+    fp = bn.engine._fast[(target, tuple(ev.keys()), N)]
+    assert _native.load().cbn_plan_flags(fp.plan.handle) & _native.CBN_PLAN_COLS
+    cap = bn.engine.fused_capacity(target, names, N)
+    assert cap >= Q > cap // 2  # two rounds of the fused grid
+    p = pdf.cpu().numpy()
+    assert p.max() == 1.0
+    bn.engine.fused = False
+    p2, _ = bn.infer(target, evt, N_max=N)
+    np.testing.assert_array_equal(p2.cpu().numpy(), p)
+    rstar = int(np.argmax(p.max(1)))
+    sub = np.append(np.append(np.arange(0, Q, Q // 40)[:40], [Q - 1]), rstar)
+    ref, _ = OracleBN(edges, cols, data).infer(target, {k: v[sub] for k, v in ev.items()}, N)
+    assert ref[-1].max() == 1.0
+    np.testing.assert_allclose(p[sub], ref, rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("d,side,Q", [(32, 5, 70001), (64, 4, 40001), (128, 4, 20001)])
 def test_slots_plan_lane_counts_rounds_and_survivors(d, side, Q, gpu):
     """k_query_slots (CBN_PLAN_SLOTS: global-table plans of >= 4 lanes per
