@@ -17,9 +17,23 @@ from . import _buildstamp
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _DEFAULT_LIB = os.path.join(_HERE, "libcbn_amd.so")
-LIB_PATH = os.environ.get("CBN_LIB_PATH") or _DEFAULT_LIB  # override: diagnostic builds
 
-ABI_VERSION = 4
+
+def lib_path() -> str:
+    """The library to load: the in-tree, stamped build -- or, only under
+    ``CBN_DIAG=1`` (the same gate as the kernel switches, include/cbn_amd.h
+    cbn_diag_enabled), a diagnostic variant named by ``CBN_LIB_PATH``.  A
+    stray ``CBN_LIB_PATH`` alone never loads an unstamped library into a
+    serving process."""
+    alt = os.environ.get("CBN_LIB_PATH")
+    if alt and os.environ.get("CBN_DIAG") == "1":
+        return alt
+    return _DEFAULT_LIB
+
+
+LIB_PATH = lib_path()
+
+ABI_VERSION = 5
 CBN_MAX_PARENTS = 8
 CBN_MAX_DIRECT_PARENTS = 32
 CBN_MAX_EVIDENCE = 256
@@ -109,6 +123,7 @@ class DirectFactor(ctypes.Structure):
         ("node_sample_idx", ctypes.c_void_p),
         ("parent_sample_idx", ctypes.c_void_p),
         ("cpd", CpdRef),
+        ("parent_ev_width", _c_int_p),  # ABI 5: 1 or N per observed parent (NULL: all 1)
     ]
 
 

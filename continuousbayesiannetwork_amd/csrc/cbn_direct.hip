@@ -48,7 +48,15 @@ struct DevDCol {             // one parent column of a direct factor
     long long stride;        // mixed-radix weight of this column
     int card;
     int ev_slot;             // evidence column or -1 (free)
+    int wide;                // observed through .expand(-1, N) from a [Q, N] column (node.py:246-248):
+                             // value i of query q is column element q * N + i, averaged like a free
+                             // parent's samples (ABI 5, cbn_direct_factor.parent_ev_width)
 };
+
+// a combo column of the free-parent mean: a free parent (its plan-time sample
+// indices) or a wide observed parent (query q's own N values, looked up in the
+// domain per combo)
+__device__ __forceinline__ bool combo_col(const DevDCol& c) { return c.ev_slot < 0 || c.wide; }
 
 struct DevDirect {
     int kind;
@@ -183,9 +191,20 @@ __global__ void k_cpd_ref_eval(DevCpd c, int n_cols, RefCols rc, const float* __
     }
 }
 
-// x_f[j] for query-independent factors (SCALAR: mean over the N node
-// samples, replicated; SHARED: mean over the N^k parent sample combos)
-__device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
+struct DEv {
+    const float* p[CBN_MAX_EVIDENCE];
+};
+
+// domain index of combo column c's sample i for query q (-1: none / off-domain)
+__device__ __forceinline__ int combo_idx(const DevDCol& c, int i, const DEv* ev, long long q, int N) {
+    return c.wide ? bsearch_dom(c.dom, c.card, ev->p[c.ev_slot][q * N + i]) : c.sample_idx[i];
+}
+
+// sum over a factor's free-parent (and wide-parent) sample combos of the CPD
+// at key base + the combo's part (query-independent factors: SHARED = mean
+// over the N^k parent sample combos; ev / q: the query, for wide parents)
+__device__ double direct_free_mean(const DevDirect& d, long long base, int N, const DEv* ev = nullptr,
+                                   long long q = 0) {
     // the combos in the reference's meshgrid order (c = 0 .. F-1, the last
     // free parent varying fastest): the outer loop forms the other free
     // parents' key part (one mixed-radix division chain per N combos), the
@@ -193,10 +212,10 @@ __device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
     // the same order as one flat loop over c, so the same fp64 sum
     int pl = -1;
     for (int p = d.n_parents - 1; p >= 0 && pl < 0; --p)
-        if (d.col[p].ev_slot < 0) pl = p;
+        if (combo_col(d.col[p])) pl = p;
     if (pl < 0) return (double)cpd_get(d.cpd, base);  // F = 1
-    const int* __restrict__ li = d.col[pl].sample_idx;
-    const long long ls = d.col[pl].stride;
+    const DevDCol& lc = d.col[pl];
+    const long long ls = lc.stride;
     const long long outer = d.free_combos / N;
     double s = 0.0;  // fp64 sum, one rounding of the mean (see entry_partial, cbn_infer.hip)
     for (long long o = 0; o < outer; ++o) {
@@ -204,9 +223,9 @@ __device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
         bool ok = true;
         for (int p = pl - 1; p >= 0; --p) {
             const DevDCol& col = d.col[p];
-            if (col.ev_slot < 0) {
+            if (combo_col(col)) {
                 const long long qq = cc / N;
-                const int pi = col.sample_idx[cc - qq * N];
+                const int pi = combo_idx(col, (int)(cc - qq * N), ev, q, N);
                 cc = qq;
                 ok &= pi >= 0;
                 key += (long long)(pi < 0 ? 0 : pi) * col.stride;
@@ -214,7 +233,7 @@ __device__ double direct_free_mean(const DevDirect& d, long long base, int N) {
         }
         if (!ok) continue;  // N terms of +0.0: s is unchanged (s >= +0)
         for (int j = 0; j < N; ++j) {
-            const int pi = li[j];
+            const int pi = combo_idx(lc, j, ev, q, N);
             s += pi >= 0 ? (double)cpd_get(d.cpd, key + (long long)pi * ls) : 0.0;
         }
     }
@@ -242,10 +261,6 @@ __global__ void k_direct_const(const DevDirect* __restrict__ fac, const int* __r
     out[i] = x;
 }
 
-struct DEv {
-    const float* p[CBN_MAX_EVIDENCE];
-};
-
 // Observed-parent part of each QUERY factor's CPD key, once per (factor,
 // query) instead of once per (query, sample column): thread per (k, q), q
 // fastest (coalesced evidence reads, wave-uniform factor).  keys[k * Q + q] =
@@ -264,7 +279,7 @@ __global__ void __launch_bounds__(kDThreads) k_direct_keys(const DevDirect* __re
         bool ok = true;
         for (int p = 0; p < d.n_parents; ++p) {
             const DevDCol& col = d.col[p];
-            if (col.ev_slot >= 0) {
+            if (col.ev_slot >= 0 && !col.wide) {
                 const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
                 ok &= idx >= 0;
                 base += (long long)(idx < 0 ? 0 : idx) * col.stride;
@@ -305,14 +320,14 @@ __global__ void __launch_bounds__(kDThreads) k_query_direct(const DevDirect* __r
                 } else {
                     for (int p = 0; p < d.n_parents; ++p) {
                         const DevDCol& col = d.col[p];
-                        if (col.ev_slot >= 0) {
+                        if (col.ev_slot >= 0 && !col.wide) {
                             const int idx = bsearch_dom(col.dom, col.card, ev.p[col.ev_slot][q]);
                             ok &= idx >= 0;
                             base += (long long)(idx < 0 ? 0 : idx) * col.stride;
                         }
                     }
                 }
-                x = ok ? (float)(direct_free_mean(d, base, N) / (double)d.free_combos) : 0.f;
+                x = ok ? (float)(direct_free_mean(d, base, N, &ev, q) / (double)d.free_combos) : 0.f;
             }
             acc = acc * x;
         }
@@ -511,9 +526,19 @@ int cbn_plan_create_direct(const cbn_direct_factor* factors, int32_t n_factors, 
             c.stride = stride[p];
             c.ev_slot = h.parent_ev_slot ? h.parent_ev_slot[p] : -1;
             if (c.ev_slot >= CBN_MAX_EVIDENCE) return set_err(CBN_E_ARG, "factor %d: evidence slot %d", f, c.ev_slot);
+            const int width = c.ev_slot >= 0 && h.parent_ev_width ? h.parent_ev_width[p] : 1;
+            if (width != 1 && width != N)
+                return set_err(CBN_E_ARG, "factor %d: parent %d evidence width %d (1 or N = %d)", f, p, width, N);
+            c.wide = width != 1 ? 1 : 0;
             if (c.ev_slot >= 0) {
                 ++d.n_obs;
                 ns = std::max(ns, c.ev_slot + 1);
+                if (c.wide) {  // N per-query values: N more combos, like a free parent
+                    if (F > kDirectThreadLookups / N)
+                        return set_err(CBN_E_LIMIT,
+                                       "factor %d: more than 2^26 parent sample combos (one thread's serial loop)", f);
+                    F *= N;
+                }
             } else {
                 if (!h.parent_sample_idx) return set_err(CBN_E_ARG, "factor %d: free parent without samples", f);
                 c.sample_idx = h.parent_sample_idx + (long long)p * N;

@@ -2579,10 +2579,11 @@ int cbn_debug_set_check_buffer(void* dev_ptr) {
 }
 #endif
 
-// Test hook: mark the plan's host-mapped status as if a fused launch had timed
-// out (the reporting path of CBN_E_TIMEOUT without starving the GPU).
+// 1 when CBN_DIAG=1 was set at load: the diagnostic CBN_* switches count.
 int32_t cbn_diag_enabled(void) { return g_diag ? 1 : 0; }
 
+// Test hook: mark the plan's host-mapped status as if a fused launch had timed
+// out (the reporting path of CBN_E_TIMEOUT without starving the GPU).
 int cbn_debug_flag_timeout(cbn_plan* plan) {
     if (!plan || !plan->h_status) return set_err(CBN_E_ARG, "cbn_debug_flag_timeout: plan has no status word");
     __atomic_store_n(plan->h_status, 1u, __ATOMIC_RELEASE);
@@ -2730,12 +2731,15 @@ int cbn_plan_create(const cbn_factor_desc* factors, int32_t n_factors, int32_t n
             long long recb = (long long)n_factors * kRecFloats * 4;  // the records go to LDS too
             if (Lp > 2 && !diag_env("CBN_NO_SLOTS")) {
                 // k_query_slots (>= 4 lanes per query) takes the plan if it can:
-                // budget the small tables beside ITS side buffers
+                // budget the small tables beside ITS side buffers -- or beside
+                // k_query_fast's side + records where those are larger, since
+                // the fast gate (below) runs first and k_query_slots may still
+                // decline the plan (a card > 32767, a row weight >= 2^24)
                 int ns_est = 0;
                 for (int f = 0; f < n_factors; ++f)
                     for (int q = 0; q < factors[f].n_parents && q < kMaxP; ++q)
                         ns_est = std::max(ns_est, factors[f].parent_ev_slot[q] + 1);
-                side = (long long)slots_lds_bytes(0, ns_est, n_factors, kQueryThreads / Lp);
+                side = std::max((long long)slots_lds_bytes(0, ns_est, n_factors, kQueryThreads / Lp), side + recb);
                 recb = 0;
             }
             long long budget = (long long)kLdsBudget - side - recb - 1024;  // bytes

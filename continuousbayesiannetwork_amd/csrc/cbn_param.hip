@@ -836,6 +836,19 @@ struct FSplit {
     int parts;
     int comb_off;
     int f[7];
+    // Order guard (round 6): each part p >= 1 multiplies its range from 1,
+    // the reference from the running product (bayesian_network.py:293).  The
+    // two agree to rounding whenever neither ever leaves the normal range;
+    // lo[p] = 2^-125 G_p and hi[p] = 2^126 / G_p, G_p = the product over part
+    // p's factors of max(1, the density's peak) -- an upper bound on any
+    // partial product of the range (cbn_param.hip param_split_guard).
+    // gs[p] = 2^-125 prod_{q >= p} G_q bounds both orders' values in a column
+    // where part p's checks fail.  mono: every peak <= 1, so every running
+    // product only falls and the final product alone decides (>= 2^-125).
+    float lo[7];
+    float hi[7];
+    float gs[7];
+    int mono;
 };
 
 // Occupancy target per instantiation (waves per SIMD the register
@@ -900,14 +913,19 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
-        const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
+        // acc *= factors [fb, fe) in order (the reference's running product).
+        // One code site for both passes: the second (the order guard's
+        // continuation, below) re-enters this loop without the barriers.
+        int fb = active ? f0 : f1, fe = f1;  // an idle wave (batch tail) skips its factors
+        bool keep = false;
+        for (bool first = true;; first = false) {
         if constexpr (!(M1 && TAB)) {  // (the M1 table loop loads its own, two factors ahead)
-            if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qb, z);
-            else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
+            if (TAB) load_inputs_tab(ev, fb < nf ? fb : nf - 1, qb, z);
+            else load_inputs(incol + (fb < nf ? fb : nf - 1) * kMaxP, qs, z);
         }
         if constexpr (M1 && TAB) {  // hot headers, one factor ahead
             const PHead* __restrict__ hd = reinterpret_cast<const PHead*>(img + cst_off + 4);
-            PHead h = hd[fa < nf ? fa : nf - 1];
+            PHead h = hd[fb < nf ? fb : nf - 1];
             // Evidence two factors ahead in two buffers used in turn (round
             // 5): no register copy at the end of a factor, and every input
             // is loaded (an input that is not evidence reads the image's 0
@@ -917,7 +935,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             // factor: the prefetch covered one factor's VALU, not a miss.)
             const float* zcell = img + cst_off;  // {0, 1}: element 0 is 0
             auto load_z = [&](int f, float (&zz)[kMaxP]) {
-                const int fi = f < f1 ? f : f1 - 1;  // (past the range: reload the last one, unused)
+                const int fi = f < fe ? f : fe - 1;  // (past the range: reload the last one, unused)
                 const PEv4 c = reinterpret_cast<const PEv4*>(ev.p)[fi > 0 ? fi : 0];
 #pragma unroll
                 for (int i = 0; i < kTabIn; ++i) zz[i] = gload_b(c.p[i] ? c.p[i] : zcell, c.p[i] ? qb : 0u);
@@ -925,7 +943,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 for (int i = kTabIn; i < kMaxP; ++i) zz[i] = 0.f;
             };
             auto eval = [&](int f, const float (&zz)[kMaxP]) {
-                const int fn = f + 1 < f1 ? f + 1 : f;
+                const int fn = f + 1 < fe ? f + 1 : f;
                 const PHead hn = hd[fn];
                 const float* R = img + h.row + col0;
                 if (h.kind != CBN_FACTOR_QUERY) {
@@ -948,21 +966,21 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 h = hn;
             };
             float zb[kMaxP];
-            load_z(fa, z);
-            load_z(fa + 1, zb);
-            for (int f = fa; f < f1; f += 2) {
+            load_z(fb, z);
+            load_z(fb + 1, zb);
+            for (int f = fb; f < fe; f += 2) {
                 eval(f, z);
                 load_z(f + 2, z);
-                if (f + 1 < f1) {
+                if (f + 1 < fe) {
                     eval(f + 1, zb);
                     load_z(f + 3, zb);
                 }
             }
         } else
-        for (int f = fa; f < f1; ++f) {
+        for (int f = fb; f < fe; ++f) {
             const PRec& r = rec[f];
             float zn[kMaxP];
-            const int fn = f + 1 < f1 ? f + 1 : f;  // next factor's evidence in flight during this one
+            const int fn = f + 1 < fe ? f + 1 : f;  // next factor's evidence in flight during this one
             if (TAB) load_inputs_tab(ev, fn, qb, zn);
             else load_inputs(incol + fn * kMaxP, qs, zn);
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
@@ -1002,7 +1020,16 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
             for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
         }
-        if (parts > 1) {
+        if (!first) {
+            if (keep) {  // a lane the guard cleared: its split product, parked in its own slot
+#pragma unroll
+                for (int j = 0; j < NC; ++j) acc[j] = comb[(wid * NC + j) * kWave + lane];
+            }
+            break;
+        }
+        if (parts == 1) break;
+        bool again = false;
+        {
             float* mine = comb + (wid * NC) * kWave + lane;
             if (part != 0 && active) {
 #pragma unroll
@@ -1010,12 +1037,65 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             }
             __syncthreads();
             if (part == 0 && active) {
-                for (int p = 1; p < parts; ++p) {
+                // The parts' products in part order, under the order guard
+                // (FSplit).  Per lane: `must` = the reference's running
+                // product may overflow where the split's does not; U bounds
+                // both orders' values in the columns where some product may
+                // have left the normal range (<= 2^-125 G_p-style bounds:
+                // gs[p] = 2^-125 prod_{q >= p} G_q).  A lane whose U is below
+                // 2^-30 of its own largest product differs by less than
+                // 2^-30 of the global max after the division (that max is at
+                // least this row's) -- it keeps the split's product; any
+                // other lane takes the reference's order: the wave continues
+                // the running product from part 0's range (the reference's
+                // prefix, bit for bit).  The decision is the row's own, so a
+                // row's bits never depend on its wave-mates (sharding).
+                // (Two passes over the LDS products -- the test, then the
+                // same multiplications -- so the test holds no second row of
+                // registers.)
+                bool must = false;
+                float U = 0.f, tmax = 0.f;
 #pragma unroll
-                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                for (int j = 0; j < NC; ++j) {
+                    float pr = acc[j];
+                    for (int p = 1; p < parts; ++p) {
+                        const float P = mine[(p * NC + j) * kWave];
+                        if (!sp.mono) {
+                            must |= j < ncol && !(pr <= sp.hi[p]);
+                            const float pn = pr * P;
+                            if (j < ncol && (!(P >= sp.lo[p]) || !(pn >= sp.lo[p]))) U = fmaxf(U, sp.gs[p] * fmaxf(1.f, pr));
+                            pr = pn;
+                        } else {
+                            pr = pr * P;
+                        }
+                    }
+                    if (sp.mono && j < ncol && !(pr >= 0x1p-125f)) U = 0x1p-125f;
+                    if (j < ncol) tmax = fmaxf(tmax, pr);
+                }
+                const bool seq = must || U > tmax * 0x1p-30f;
+                if (__builtin_expect(__any(seq), 0)) {
+                    if (!seq) {
+                        for (int p = 1; p < parts; ++p) {
+#pragma unroll
+                            for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                        }
+#pragma unroll
+                        for (int j = 0; j < NC; ++j) mine[j * kWave] = acc[j];  // (own slot: free)
+                    }
+                    keep = !seq;
+                    fb = sp.f[1];
+                    fe = sp.f[parts];
+                    again = true;
+                } else {
+                    for (int p = 1; p < parts; ++p) {
+#pragma unroll
+                        for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                    }
                 }
             }
             __syncthreads();
+        }
+        if (!again) break;
         }
         if (part == 0 && active && valid) {
             float* o = out + q * N + col0;
@@ -1472,6 +1552,9 @@ struct ParamPlan {
     size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
     int split[7][8] = {};  // factor ranges for 1, 2, 3, 4 and 6 parts (index: parts)
+    float guard_lo[7][8] = {}, guard_hi[7][8] = {}, guard_gs[7][8] = {};  // order guard per split (FSplit)
+    bool guard_ok[7] = {};  // every part's bound G_p <= 2^100 (else the plan runs 1 part)
+    bool mono = false;      // every density's peak <= 1
     float* d_image = nullptr;
     int* d_which = nullptr;
     int image_floats = 0;
@@ -1490,6 +1573,12 @@ void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long
     memset(&sp, 0, sizeof(sp));
     sp.parts = parts;
     for (int p = 0; p <= parts; ++p) sp.f[p] = pp->split[parts][p];
+    for (int p = 0; p < parts; ++p) {
+        sp.lo[p] = pp->guard_lo[parts][p];
+        sp.hi[p] = pp->guard_hi[parts][p];
+        sp.gs[p] = pp->guard_gs[parts][p];
+    }
+    sp.mono = pp->mono ? 1 : 0;
     size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
     lds = (lds + 15) & ~(size_t)15;
     sp.comb_off = (int)(lds / sizeof(float));
@@ -1593,6 +1682,7 @@ int cbn::param_run(cbn_plan* plan, int64_t n_queries, const float* const* eviden
         const int v = atoi(e);
         if (v == 1 || v == 2 || v == 3 || v == 4 || v == 6) parts = v;
     }
+    if (!pp->guard_ok[parts]) parts = 1;  // a range whose products could overflow: the reference's order only
     const int wpb = query_block_threads(parts) / kWave;
     long long grid = (waves * parts + wpb - 1) / wpb;
     grid = std::max(1LL, std::min(grid, (long long)pp->max_slots));
@@ -1748,6 +1838,45 @@ int create_param_generic(const cbn_param_factor* factors, int n_factors, int N, 
     *plan = P;
     return CBN_OK;
 }
+// The split query kernel's order guard (FSplit).  peak_f bounds factor f's
+// values: a Gaussian density's norm (linear_regression.py:91-95), a logistic
+// density's 1 / (4 scale) (logistIc_regression.py:90-98), with 2^-10 slack
+// for the rounding of the fp32 forms; a mean over free combos or a
+// query-independent row is a mean of such values.  G_p = prod over part p of
+// max(1, peak_f) bounds every partial product of the range; with G_p <=
+// 2^100 the split is kept and the kernel checks, per lane and column, that
+// the range's product and the reference's running product through part p
+// stayed within [2^-125, 2^126] -- a lane that fails and whose failing
+// columns are not provably below 2^-30 of its own largest value takes the
+// reference's order (the kernel's combine step).
+void param_split_guard(cbn::ParamPlan* pp, const PRec* recs, int n_factors) {
+    std::vector<double> peak(n_factors);
+    bool mono = true;
+    for (int f = 0; f < n_factors; ++f) {
+        const PRec& r = recs[f];
+        const double pk = (r.family == CBN_FAMILY_GAUSS ? (double)r.norm : 0.25 / (double)r.scale) * (1.0 + 0x1p-10);
+        peak[f] = pk == pk ? pk : HUGE_VAL;  // a NaN parameter: no bound
+        mono = mono && peak[f] <= 1.0;
+    }
+    pp->mono = mono;
+    for (int parts : {1, 2, 3, 4, 6}) {
+        const int* b = pp->split[parts];
+        bool ok = true;
+        double Gs = 1.0;  // prod_{q >= p} G_q
+        for (int p = parts - 1; p >= 0; --p) {
+            double G = 1.0;
+            for (int f = b[p]; f < b[p + 1]; ++f) G *= std::max(1.0, peak[f]);
+            ok = ok && G <= 0x1p100;
+            Gs *= G;
+            pp->guard_lo[parts][p] = ok ? (float)(0x1p-125 * G) : 0.f;
+            pp->guard_hi[parts][p] = ok ? (float)(0x1p126 / G) : 0.f;
+            // (beyond the float range: +inf, no lane keeps the split there)
+            pp->guard_gs[parts][p] = 0x1p-125 * Gs <= 0x1p127 ? (float)(0x1p-125 * Gs) : HUGE_VALF;
+        }
+        pp->guard_ok[parts] = parts == 1 || ok;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1924,6 +2053,7 @@ int cbn_plan_create_param(const cbn_param_factor* factors, int32_t n_factors, in
             }
             while (p <= parts) b[p++] = n_factors;
         }
+        param_split_guard(pp, recs.data(), n_factors);
     }
     cbn_plan* P = new cbn_plan();
     P->param = pp;

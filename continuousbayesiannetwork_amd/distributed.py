@@ -463,7 +463,10 @@ class ShardedStepper:
         if res is None:  # dtype / device / layout the native checks reject: convert, same ring
             # (shape errors first, as the reference raises them; no step is
             # enqueued for a malformed batch)
-            eng.check_columns(fp.plan, evidence_shard)
+            if eng.check_columns(fp.plan, evidence_shard):
+                raise NotImplementedError(
+                    "ShardedStepper takes [n_queries, 1] evidence columns; [n_queries, N_max] columns (per-query "
+                    "sample values, node.py:246-248) go through sharded_infer")
             cols = {k: evidence_shard[k] for k in fp.slot_keys}
             conv = {k: v.to(device=fp.device, dtype=torch.float32).contiguous() for k, v in cols.items()}
             res = native_step(conv)

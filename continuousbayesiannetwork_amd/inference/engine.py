@@ -245,6 +245,8 @@ class InferenceEngine:
         self.bn = bn
         self.cache_tables = cache_tables
         self._plans: Dict[tuple, Plan] = {}
+        # (target, observed, N, wide columns) -> (base plan, its direct plan for [Q, N] columns)
+        self._wide_plans: Dict[tuple, tuple] = {}
         self._orders: Dict[str, List[str]] = {}
         # record HIP events around the two query passes inside the library
         # (bench.py's per-kernel timing; read back with timing())
@@ -319,7 +321,10 @@ class InferenceEngine:
         self.epoch += 1
         for p in self._plans.values():
             p.destroy()
+        for _, wp in self._wide_plans.values():
+            wp.destroy()
         self._plans = {}
+        self._wide_plans = {}
         self._orders = {}
         self._fast = {}
 
@@ -338,6 +343,8 @@ class InferenceEngine:
         try:
             for p in self._plans.values():
                 p.destroy()
+            for _, wp in self._wide_plans.values():
+                wp.destroy()
         except Exception:
             pass
 
@@ -396,18 +403,25 @@ class InferenceEngine:
         plan.reusable = True
         plan.max_bits = torch.zeros(1, dtype=torch.int32, device=device)
 
-    def _materialise_direct(self, plan: Plan, device: torch.device):
+    def _materialise_direct(self, plan: Plan, device: torch.device, widths: Optional[Dict[str, int]] = None,
+                            share_idx: Optional[Plan] = None):
         """cbn_direct_factor per ancestor (include/cbn_amd.h): each factor is
         evaluated per (query, sample column) from its CPD -- dense or hashed --
         with no per-plan table (nodes with > 8 parents, hashed CPDs of
         continuous / high-cardinality columns, factor tables beyond the
-        table path's limits).  Same sample-index conventions as the table path."""
+        table path's limits).  Same sample-index conventions as the table path.
+        ``widths``: evidence columns taken as [Q, N] (_wide_plan);
+        ``share_idx``: a plan of the same factors whose sample-index arrays
+        this one reads (free-parent rows only, the same in both conventions)."""
         lib = _native.load()
         descs = (_native.DirectFactor * len(plan.factors))()
         keep = []
         slot_of = {v: i for i, v in enumerate(plan.slots)}
         N = plan.n_samples
-        self._alloc_index_arrays(plan, device)
+        if share_idx is None:
+            self._alloc_index_arrays(plan, device)
+        else:
+            plan.idx_flat, plan.idx_offs = share_idx.idx_flat, share_idx.idx_offs
         keep.append(plan.idx_flat)
         with torch.cuda.device(device):
             for f, spec in enumerate(plan.factors):
@@ -434,13 +448,21 @@ class InferenceEngine:
                     ref, host = est.cpd_ref()
                 d.cpd = ref
                 keep += [host, est.cpd, est.hash_keys, est.hash_vals, est.node_marginal, *doms]
-                nidx, pidx = self._index_arrays(plan, f, doms, -1)
+                if share_idx is None:
+                    nidx, pidx = self._index_arrays(plan, f, doms, -1)
+                else:
+                    nidx, pidx = self._index_views(plan.idx_flat, *plan.idx_offs[f], N)
                 d.node_sample_idx = nidx.data_ptr()
                 if k:
                     ev = (ctypes.c_int32 * k)(*[slot_of[p] if p in spec.observed else -1 for p in spec.parents])
                     keep.append(ev)
                     d.parent_ev_slot = ctypes.cast(ev, ctypes.POINTER(ctypes.c_int32))
                     d.parent_sample_idx = pidx.data_ptr()
+                    if widths:
+                        w = (ctypes.c_int32 * k)(*[widths.get(p, 1) if p in spec.observed else 1
+                                                   for p in spec.parents])
+                        keep.append(w)
+                        d.parent_ev_width = ctypes.cast(w, ctypes.POINTER(ctypes.c_int32))
             handle = ctypes.c_void_p()
             torch.cuda.current_stream(device).synchronize()  # index arrays ready before the plan reads them
             _native.check(lib.cbn_plan_create_direct(descs, len(plan.factors), N, ctypes.byref(handle)),
@@ -628,11 +650,11 @@ class InferenceEngine:
 
         A width-N column read only through ``.expand`` is accepted by the
         reference as N per-sample values of the observed parent (a per-query
-        free parent); the kernels read element q of a column as query q's
-        value, so this engine raises NotImplementedError for it instead of
-        misreading it (Parity)."""
+        free parent): those columns are returned (a set, empty when every
+        column is [Q, 1]) and run on a direct plan that averages over them
+        (``_wide_plan``; cbn_direct_factor.parent_ev_width, ABI 5)."""
         N = plan.n_samples
-        width_n = None
+        wide = set()
         for spec in plan.factors:
             if not spec.observed:
                 continue
@@ -652,12 +674,8 @@ class InferenceEngine:
                     raise RuntimeError(f"The expanded size of the tensor ({target}) must match the existing size "
                                        f"({k}) at non-singleton dimension 1.  Target sizes: {shape}.  "
                                        f"Tensor sizes: [{t.shape[0]}, {k}]")
-                width_n = width_n or p
-        if width_n is not None:
-            raise NotImplementedError(
-                f"evidence column {width_n!r} has shape [Q, {N}] (= N_max): the reference reads it as {N} "
-                f"per-sample values of a partially observed parent; this engine takes [n_queries, 1] evidence "
-                f"columns only")
+                wide.add(p)
+        return wide
 
     def _columns(self, plan: Plan, evidence, n_queries: int, device) -> List[torch.Tensor]:
         cols = []
@@ -665,8 +683,10 @@ class InferenceEngine:
             t = evidence[v]
             assert t.dim() == 2, ValueError("Each query tensor must be of dimension 2.")
             assert t.shape[0] == n_queries, ValueError("n_queries must be equal for all features.")
-            if t.shape[1] != 1:
-                self.check_columns(plan, evidence)  # raises (the reference's error, in its order)
+            if t.shape[1] != 1 and self.check_columns(plan, evidence):  # (raises the reference's errors)
+                raise NotImplementedError(
+                    "[n_queries, N_max] evidence columns run on a direct plan's raw launch (infer / infer_raw / "
+                    "sharded_infer's raw path); the two-pass passes take [n_queries, 1] columns")
             if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
                 t = t.to(device=device, dtype=torch.float32).contiguous()
             cols.append(t)
@@ -813,6 +833,9 @@ class InferenceEngine:
         n = next(iter(evidence.values())).shape[0]
         if n == 0 or (not plan.target_observed and n != 1):
             return None
+        wide = self._wide(plan, evidence)
+        if wide:  # the wide direct plan's raw launch; its max folded into words[0]
+            return self._run_wide(plan, evidence, wide, n, fp.device, out, words=words)
         cols = self._columns(plan, evidence, n, fp.device)
         if out is None:
             out = torch.empty((n, plan.n_samples), dtype=torch.float32, device=fp.device)
@@ -944,7 +967,87 @@ class InferenceEngine:
             tot[2] += b.value * n.value
         return tot[0], (tot[1] / tot[0] if tot[0] else 0.0), (tot[2] / tot[0] if tot[0] else 0.0)
 
+    def _wide(self, plan: Plan, evidence) -> set:
+        """The columns of this call read as [Q, N] per-query sample values
+        (check_columns; the reference's shape errors raise here)."""
+        for v in plan.slots:
+            t = evidence[v]
+            if t.dim() == 2 and t.shape[1] != 1:
+                return self.check_columns(plan, evidence)
+        return set()
+
+    def _wide_plan(self, plan: Plan, wide, device) -> Plan:
+        """The direct plan of ``plan`` whose observed parents in ``wide`` take
+        [Q, N] columns (node.py:246-248: each query's N values of that parent
+        enter the meshgrid like a free parent's samples, node.py:335-375, and
+        the factor is their mean).  It shares ``plan``'s sample-index arrays
+        (a redrawn plan's draws of this call included; its constant rows are
+        then rebuilt per call).  BruteForce networks only."""
+        if plan.direct is False and any(hasattr(self.bn.nodes_obj[s.node].estimator, "model_desc")
+                                        for s in plan.factors):
+            raise NotImplementedError(
+                "[n_queries, N_max] evidence columns (per-query sample values, node.py:246-248) are evaluated on "
+                "BruteForce networks; the parametric kernels take [n_queries, 1] columns")
+        key = (plan.target, plan.observed, plan.n_samples, frozenset(wide))
+        wp = self._wide_plans.get(key)
+        if wp is not None and wp[0] is plan:
+            return wp[1]
+        import dataclasses
+
+        wp = dataclasses.replace(plan, handle=None, keep=[], max_bits=None, tables_built=False, direct=False,
+                                 redraw=None, idx_host=None)
+        self._materialise_direct(wp, device, widths={c: plan.n_samples for c in wide}, share_idx=plan)
+        wp.words = torch.zeros(int(_native.load().cbn_plan_max_words(wp.handle)), dtype=torch.int32, device=device)
+        old = self._wide_plans.pop(key, None)
+        if old is not None:
+            torch.cuda.synchronize()
+            old[1].destroy()
+        self._wide_plans[key] = (plan, wp)
+        return wp
+
+    def _run_wide(self, plan: Plan, evidence, wide, n_queries: int, device, out, words=None):
+        """One call with [Q, N] columns on the wide direct plan: raw launch,
+        then (words None) the global-max division; else the launch's max
+        folded into words[0] (the caller's exchange / scale)."""
+        wp = self._wide_plan(plan, wide, device)
+        N = plan.n_samples
+        cols = []
+        for v in plan.slots:
+            t = evidence[v]
+            if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(device=device, dtype=torch.float32).contiguous()
+            cols.append(t)
+        tq = n_queries if plan.target_observed else 1
+        tdom = plan.target_domain.unsqueeze(0).expand(tq, -1)
+        if (n_queries, N) != tuple(tdom.shape):
+            raise AssertionError("pdf and domain must have same shape.")
+        if n_queries == 0:
+            raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")
+        if out is None:
+            out = torch.empty((n_queries, N), dtype=torch.float32, device=device)
+        flags = _native.CBN_RUN_RAW
+        if not wp.tables_built or not plan.deterministic:  # (a redrawn plan's constant rows: this call's draws)
+            flags |= _native.CBN_RUN_BUILD_TABLES
+            wp.tables_built = True
+        ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+        lib = _native.load()
+        with torch.cuda.device(device):
+            s = _native.stream_ptr(device)
+            _native.check(lib.cbn_plan_run(wp.handle, n_queries, ptrs, len(cols), _native.ptr(wp.words),
+                                           _native.ptr(out), flags, s), "cbn_plan_run(wide)")
+            if words is not None:
+                # non-negative floats (NaN propagating, as torch.max): the max of the block words
+                words.zero_()
+                words[:1] = wp.words.view(torch.float32).max().reshape(1).view(torch.int32)
+                return out
+            _native.check(lib.cbn_scale(_native.ptr(out), n_queries * N, _native.ptr(wp.words), wp.words.numel(), s),
+                          "cbn_scale")
+        return out, tdom
+
     def _run(self, plan: Plan, evidence, n_queries: int, device, out):
+        wide = self._wide(plan, evidence)
+        if wide:
+            return self._run_wide(plan, evidence, wide, n_queries, device, out)
         lib = _native.load()
         N = plan.n_samples
         cols = self._columns(plan, evidence, n_queries, device)

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define CBN_AMD_ABI_VERSION 4
+#define CBN_AMD_ABI_VERSION 5
 
 #define CBN_MAX_PARENTS 8    /* parents per node handled by one factor descriptor */
 #define CBN_MAX_EVIDENCE 256 /* distinct evidence columns per query batch        */
@@ -53,7 +53,14 @@ typedef struct cbn_factor_desc {
     int32_t parent_card[CBN_MAX_PARENTS];         /* |domain(parent_i)|                  */
     int32_t parent_ev_slot[CBN_MAX_PARENTS];      /* -1: free parent; else evidence col  */
     const float* cpd;                             /* dense CPD [parent_card..., node_card]
-                                                     (root: marginal [node_card])        */
+                                                     (root: marginal [node_card]); every
+                                                     entry finite and >= 0 (BruteForce's
+                                                     joint / (marginal + 1e-10) always
+                                                     is): the table kernels stop
+                                                     multiplying a query's row once it
+                                                     is all +0, which equals the
+                                                     reference's product only when no
+                                                     later factor is inf (0 x inf = NaN) */
     const int32_t* node_sample_idx;               /* [N] node sample -> domain idx or -1 */
     const int32_t* parent_sample_idx;             /* [k*N] free-parent sample idx or -1  */
     const float* parent_domain[CBN_MAX_PARENTS];  /* sorted domain values (observed parents) */
@@ -135,6 +142,14 @@ typedef struct cbn_direct_factor {
     const int32_t* node_sample_idx;   /* device [N]: node sample -> domain idx or -1    */
     const int32_t* parent_sample_idx; /* device [k*N]: free-parent sample idx or -1     */
     cbn_cpd_ref cpd;                  /* columns: parents..., node                      */
+    /* host [k] or NULL (all 1): the width of each observed parent's evidence
+     * column -- 1, or N_max for a [n_queries, N_max] column that the node reads
+     * through Node._setup_parents_query's .expand(-1, N) (node.py:246-248: a
+     * node whose evidence keys are not all its parents) as N per-query sample
+     * values of that parent; element (q, i) of such a column is value i of
+     * query q, and the factor averages over them like a free parent's samples
+     * (node.py:335-375).  Added in ABI 5 (round 6). */
+    const int32_t* parent_ev_width;
 } cbn_direct_factor;
 
 /* A plan whose factors are evaluated directly (BayesianNetwork.infer,

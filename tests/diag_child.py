@@ -8,6 +8,7 @@ the environment it is testing.  Prints one JSON line.
     python tests/diag_child.py enabled   # no GPU: cbn_diag_enabled()
     python tests/diag_child.py flags     # configs[1]-shaped plan's cbn_plan_flags
     python tests/diag_child.py generic   # NN [16] rows: fast kernel vs CBN_PARAM_GENERIC
+    python tests/diag_child.py gridfull  # configs[4] bench batch: k_query_slots vs k_query_fast (CBN_NO_SLOTS)
 """
 import json
 import os
@@ -58,6 +59,24 @@ def main(mode: str):
             outs.append(bn.infer(cols[-1], ev, N_max=8)[0].cpu().numpy())
         res["equal"] = bool(np.array_equal(outs[0], outs[1], equal_nan=True))
         res["finite"] = int(np.isfinite(outs[0]).sum())
+    elif mode == "gridfull":
+        # tools/bench_grid.py's headline batch (BASELINE configs[4], 65 536 queries)
+        from helpers import grid_data
+
+        data, cols, edges = grid_data(400_000, 3, side=10, d=64, keep=0.995, noise=0)
+        target, names = cols[-1], cols[:-1]
+        ev = {k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, 65536, 0).items()}
+        bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
+        outs, flags = [], []
+        for no_slots in (False, True):
+            if no_slots:  # read at plan creation: drop the cached plan
+                os.environ["CBN_NO_SLOTS"] = "1"
+                bn.engine.invalidate()
+            outs.append(bn.infer(target, ev, N_max=64)[0].cpu().numpy())
+            flags += [int(lib.cbn_plan_flags(p.handle)) for p in bn.engine._plans.values()]
+        res["flags"] = flags
+        res["equal"] = bool(np.array_equal(outs[0], outs[1], equal_nan=True))
+        res["nonzero_rows"] = int((outs[0] > 0).any(1).sum())
     print(json.dumps(res))
 
 

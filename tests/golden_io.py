@@ -31,8 +31,8 @@ def golden_error(meta):
 
 def width_n_only(meta):
     """A fixture whose evidence has [Q, N] columns that the reference reads
-    through ``.expand(-1, N)`` only (node.py:246-248) -- accepted by the
-    reference, NotImplementedError in the HIP engine (Parity)."""
+    through ``.expand(-1, N)`` only (node.py:246-248): N per-query sample
+    values of that parent (the engine's wide direct plan, round 6)."""
     return not meta["error"] and any(k != 1 for k in meta.get("width", {}).values())
 
 

@@ -43,3 +43,13 @@ def test_generic_kernel_equals_fast_kernel(gpu):
     test_gpu_param.py: the switch is read at plan creation, the gate at load)."""
     res, _ = _child("generic", CBN_DIAG="1")
     assert res["diag"] == 1 and res["equal"] and res["finite"] > 0
+
+
+def test_grid_bench_batch_slots_equals_fast_kernel(gpu):
+    """configs[4] at its benchmarked size (tools/bench_grid.py's headline
+    batch: 100 factors, L = 8, 65 536 queries -- k_query_slots' fused
+    two-round launch with a 3-chunk phase-B survivor chain) == k_query_fast
+    (CBN_NO_SLOTS=1 under CBN_DIAG=1) bit for bit."""
+    res, _ = _child("gridfull", CBN_DIAG="1")
+    assert res["diag"] == 1 and res["equal"] and res["nonzero_rows"] > 1000
+    assert res["flags"][0] & _native.CBN_PLAN_SLOTS and not res["flags"][1] & _native.CBN_PLAN_SLOTS

@@ -26,7 +26,8 @@ pytestmark = pytest.mark.gpu
 RTOL, ATOL = 1e-5, 1e-7
 DIRECT_GOLDENS = ["wide10_free2", "wide12_all", "hicard40_all", "hicard40_free1", "cont4_all", "cont4_free1",
                   "cont4_free_support"]
-OK_GOLDENS = [n for n in golden_names() if not load_golden(n)["meta"]["error"] and not width_n_only(load_golden(n)["meta"])]
+OK_GOLDENS = [n for n in golden_names() if not load_golden(n)["meta"]["error"]]
+WIDE_GOLDENS = [n for n in OK_GOLDENS if width_n_only(load_golden(n)["meta"])]
 
 
 def _t(ev, dev):
@@ -230,3 +231,81 @@ def test_direct_free_combos_beyond_2_20_and_the_call_bound(gpu):
     bn.engine.force_direct = True
     with pytest.raises(_native.NativeError, match=r"2\^26"):
         bn.infer("Y", {}, N_max=d)
+
+
+# ---------------------------------------------------------------------------
+# [Q, N] evidence columns read through .expand (round 6).  A node whose
+# evidence keys are not all its parents expands each observed column to
+# [Q, N] (node.py:246-248); a width-N column is then N per-query sample values
+# of that parent, entering the meshgrid like a free parent's samples
+# (node.py:335-375), and the factor is the mean over all the combos
+# (bayesian_network.py:292).  The engine runs such calls on a direct plan
+# whose wide parents read their values per (query, combo)
+# (cbn_direct_factor.parent_ev_width, ABI 5).
+def _wide_net(S=6000, seed=3, d=4):
+    rng = np.random.default_rng(seed)
+    A = rng.integers(0, d, S)
+    B = rng.integers(0, d, S)
+    C = (A + B + rng.integers(0, 2, S)) % d
+    D = (A + rng.integers(0, 2, S)) % d
+    E = (C + D + rng.integers(0, 2, S)) % d
+    data = np.stack([A, B, C, D, E], 1).astype(np.float32)
+    cols = ["A", "B", "C", "D", "E"]
+    edges = [("A", "C"), ("B", "C"), ("C", "E"), ("D", "E"), ("A", "D")]
+    return data, cols, edges
+
+
+@pytest.mark.parametrize("name", WIDE_GOLDENS)
+def test_wide_golden_raw_and_sharded_paths(name, gpu):
+    """The reference's own [Q, N] fixture (multi_widthN_partial) through the
+    raw launch + scale (sharded_infer, no process group) as well as infer."""
+    from continuousbayesiannetwork_amd.distributed import sharded_infer
+
+    bn, pdf = _run_golden(name, gpu)
+    m = load_golden(name)["meta"]
+    g = load_golden(name)
+    ev = _t({k: g["evidence"][k] for k in m["evidence"]}, gpu)
+    random.seed(m["seed"])
+    two, _ = sharded_infer(bn, m["target"], ev, N_max=m["N_max"])
+    np.testing.assert_array_equal(two.cpu().numpy(), pdf.cpu().numpy())
+
+
+@pytest.mark.parametrize("N,Q", [(4, 3000), (3, 257), (6, 999)])
+def test_wide_columns_match_oracle(N, Q, gpu):
+    """E's parents C, D with evidence on C only (the expand path): C given as
+    [Q, N] per-query values (some off the domain), plus D free -- N x N combos
+    per query; A -> C and A -> D give the other factors.  N = 6 > |domain| = 4:
+    the redrawn sample domains (node.py:302-333) of the same call, drawn in the
+    reference's order.  infer, the repeat call (cached wide plan) and the raw
+    path match the oracle; the [Q, 1] call on the same engine still takes its
+    own plan.  ShardedStepper declines [Q, N] columns (NotImplementedError)."""
+    from continuousbayesiannetwork_amd.distributed import ShardedStepper, sharded_infer
+
+    data, cols, edges = _wide_net()
+    rng = np.random.default_rng(N * 7 + Q)
+    cw = rng.integers(0, 4, (Q, N)).astype(np.float32)
+    cw[::17, 0] = 9.0  # off the fitted domain: that combo's pdf is 0
+    ev = {"C": cw}
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    for _ in range(2):
+        random.seed(11)
+        ref, rdom = ora.infer("E", ev, N)
+        random.seed(11)
+        pdf, dom = bn.infer("E", _t(ev, gpu), N_max=N)
+        np.testing.assert_array_equal(dom.cpu().numpy(), rdom)
+        np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    random.seed(11)
+    two, _ = sharded_infer(bn, "E", _t(ev, gpu), N_max=N)
+    np.testing.assert_allclose(two.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    ev1 = {"C": cw[:, :1].copy()}
+    random.seed(12)
+    ref1, _ = ora.infer("E", ev1, N)
+    random.seed(12)
+    pdf1, _ = bn.infer("E", _t(ev1, gpu), N_max=N)
+    np.testing.assert_allclose(pdf1.cpu().numpy(), ref1, rtol=RTOL, atol=ATOL)
+    if N <= 4:  # deterministic plans: the pipelined stepper
+        st = ShardedStepper(bn, "E", N)
+        with pytest.raises(NotImplementedError):
+            st.step(_t(ev, gpu))
+        st.close()

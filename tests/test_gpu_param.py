@@ -463,3 +463,104 @@ def test_subnormal_densities_in_infer(gpu):
     np.testing.assert_allclose(raw, ref_raw, rtol=RTOL, atol=2.0 ** -146)
     scale(rows, words)
     np.testing.assert_allclose(rows.cpu().numpy(), ref_raw / ref_raw.max(), rtol=RTOL, atol=ATOL)
+
+
+# ---------------------------------------------------------------------------
+# Order guard of the factor split (round 6).  The M1 linear kernels multiply
+# the factors in 4 contiguous ranges from 1 and then multiply the ranges
+# together; the reference keeps ONE running product (bayesian_network.py:269,
+# :293).  Where a range's own product under- or overflows while the running
+# product does not (or the reverse), the orders give different numbers; the
+# kernel then recomputes that wave in the reference's order (cbn_param.hip,
+# FSplit).  24-node LinearRegression chain, N = 16 = every node's domain
+# {0.0, 0.1, ..., 1.5}: the plan splits its 24 factors [0, 7) [7, 13) [13, 19)
+# [19, 24) (the host's cost balance: root 1, each query factor 242).
+_GUARD_N = 24
+_GUARD_DOM = (np.arange(16) * 0.1).astype(np.float32)
+
+
+def _guard_chain(gpu, sigmas):
+    rng = np.random.default_rng(61)
+    cols = [f"X{i}" for i in range(_GUARD_N)]
+    edges = [(cols[i], cols[i + 1]) for i in range(_GUARD_N - 1)]
+    data = _GUARD_DOM[rng.integers(0, 16, (2000, _GUARD_N))]
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu, estimator="linear_regression",
+                 config=param_config("linear_regression", n_epochs=1))
+    _set_linear(bn.nodes_obj["X0"].estimator, [[0.0]], [0.7], 0.0, gpu)
+    for i in range(1, _GUARD_N):  # mu = the parent's evidence
+        _set_linear(bn.nodes_obj[cols[i]].estimator, [[1.0]], [0.0], float(np.log(sigmas[i])), gpu)
+    ora = _oracle_from_bn(bn, edges, cols, data, "linear_regression")
+    return bn, ora, cols
+
+
+def _guard_evidence(cols, Q, offsets):
+    """Evidence of X0..X22: X_{i-1} = s_7 + offsets[i] (query-dependent rows of offsets)."""
+    ev = {}
+    for i in range(1, _GUARD_N):
+        ev[cols[i - 1]] = (_GUARD_DOM[7] + offsets[i]).astype(np.float32)[:, None]
+    return ev
+
+
+def _guard_check(bn, ora, ev, gpu):
+    rows, _, words, scale = bn.engine.infer_raw(cols_target := f"X{_GUARD_N - 1}", _t(ev, gpu), 16)
+    raw = rows.cpu().numpy().copy()
+    with np.errstate(over="ignore", invalid="ignore", under="ignore"):
+        ref_raw, _ = ora.infer_raw(cols_target, ev, 16)
+        ref = ref_raw / ref_raw.max()
+    np.testing.assert_array_equal(np.isnan(raw), np.isnan(ref_raw))
+    np.testing.assert_array_equal(np.isinf(raw), np.isinf(ref_raw))
+    fin = np.isfinite(ref_raw)
+    np.testing.assert_allclose(raw[fin], ref_raw[fin], rtol=RTOL, atol=2.0 ** -146)
+    scale(rows, words)
+    out = rows.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+    np.testing.assert_allclose(out, ref, rtol=RTOL, atol=ATOL, equal_nan=True)
+    pdf, _ = bn.infer(cols_target, _t(ev, gpu), N_max=16)  # the fused / two-pass path too
+    np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL, equal_nan=True)
+    return ref_raw
+
+
+def test_split_order_guard_range_underflow(gpu):
+    """Part 0's six sharp factors (sigma 1e-4, evidence at the mean: 3989 each)
+    lift the running product to ~1e21; part 1's six factors sit 7.2-7.4 sigma
+    off (~1e-8 each): that range's product alone (~1e-48) flushes to 0, the
+    reference's running product (~1e-27) stays normal.  Unguarded, the split
+    returned 0 for every row's only nonzero column."""
+    sig = [1.0] + [1e-4] * 12 + [1.0] * (_GUARD_N - 13)
+    bn, ora, cols = _guard_chain(gpu, sig)
+    Q = 4096
+    rng = np.random.default_rng(5)
+    off = np.zeros((_GUARD_N, Q), np.float32)
+    off[7:13] = rng.uniform(7.2e-4, 7.4e-4, (6, Q)).astype(np.float32)  # parts 1's factors X7..X12
+    ref_raw = _guard_check(bn, ora, _guard_evidence(cols, Q, off), gpu)
+    P1 = np.prod([3989.4 * np.exp(-0.5 * (off[i] / 1e-4) ** 2) for i in range(7, 13)], axis=0)
+    assert (P1 < 2.0 ** -149).all() and (ref_raw[:, 7] > 2.0 ** -120).all()  # the case is exercised
+
+
+def test_split_order_guard_running_overflow(gpu):
+    """The mirror: the reference's running product overflows inside part 1
+    (1e21 x 3989^5 > FLT_MAX) and stays inf -- its max is inf, so those rows
+    normalise to NaN and every finite row to 0 -- while part 1's own range
+    (3989^5 x 1e-11) and the split's product stay finite.  Half the queries
+    overflow; the other half keep part 1 far off its mean (finite rows)."""
+    sig = [1.0] + [1e-4] * 12 + [1.0] * (_GUARD_N - 13)
+    bn, ora, cols = _guard_chain(gpu, sig)
+    Q = 2048
+    off = np.zeros((_GUARD_N, Q), np.float32)
+    off[12] = 8.0e-4  # X12 (last of part 1): 3989 e^-32
+    off[8:12, Q // 2:] = 6.0e-4  # the finite half: X8..X11 at 6 sigma
+    ref_raw = _guard_check(bn, ora, _guard_evidence(cols, Q, off), gpu)
+    assert np.isinf(ref_raw[: Q // 2, 7]).all() and np.isfinite(ref_raw[Q // 2:]).all()
+
+
+def test_split_order_guard_quiet_case(gpu):
+    """Every range and every running product normal (parts 1.. near their
+    means): the split's products are kept, and agree with the reference's
+    order to the north-star tolerance on every row."""
+    sig = [1.0] + [0.05] * 12 + [1.0] * (_GUARD_N - 13)
+    bn, ora, cols = _guard_chain(gpu, sig)
+    Q = 4096
+    rng = np.random.default_rng(8)
+    off = rng.uniform(-0.02, 0.02, (_GUARD_N, Q)).astype(np.float32)
+    ref_raw = _guard_check(bn, ora, _guard_evidence(cols, Q, off), gpu)
+    assert (ref_raw[:, 7] > 2.0 ** -100).all()

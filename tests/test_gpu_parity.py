@@ -39,10 +39,6 @@ def test_infer_matches_reference_golden(name, gpu):
             if exc is RuntimeError:  # evidence widths: the reference's message too
                 assert str(info.value) == msg
         return
-    if width_n_only(m):
-        with pytest.raises(NotImplementedError):
-            bn.infer(m["target"], ev, N_max=m["N_max"])
-        return
     pdf, dom = bn.infer(m["target"], ev, N_max=m["N_max"])
     assert pdf.device.type == "cuda"
     np.testing.assert_array_equal(dom.cpu().numpy(), g["domain"])
@@ -586,6 +582,48 @@ def test_grid_full_config4_shape_matches_reference_and_oracle(gpu):
     np.testing.assert_allclose(out, zr["pdf"], rtol=RTOL, atol=ATOL)
     one, _ = sharded_infer(bn, target, ev, N_max=64)
     np.testing.assert_array_equal(one.cpu().numpy(), out)
+
+
+def test_grid_bench_batch_full_size(gpu):
+    """configs[4] at the size it is benchmarked at (tools/bench_grid.py's
+    headline batch: 10 x 10 grid, d = N = 64, 100 factors, 65 536 queries --
+    k_query_slots' fused launch over two block rounds, round 0's products
+    held across the grid barrier, phase B a 3-chunk survivor chain): fused ==
+    raw launch + scale (two launches) bit for bit; the UNnormalised rows of
+    40 sampled rows, the first and last 128-query block and the batch argmax
+    row vs the oracle (tests/golden/make_grid_bench_oracle.py) at rtol 1e-5,
+    and the normalised rows vs those over the GPU's max."""
+    import os
+
+    from continuousbayesiannetwork_amd import _native
+    from continuousbayesiannetwork_amd.distributed import sharded_infer
+
+    from helpers import grid_data
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "grid10_d64_bench65536_oracle.npz"))
+    data, cols, edges = grid_data(400_000, 3, side=10, d=64, keep=0.995, noise=0)
+    target, names = cols[-1], cols[:-1]
+    ev = _t(sample_evidence(data, cols, names, 65536, 0), gpu)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    pdf, dom = bn.infer(target, ev, N_max=64)
+    fp = bn.engine._fast[(target, tuple(ev.keys()), 64)]
+    assert _native.load().cbn_plan_flags(fp.plan.handle) & _native.CBN_PLAN_SLOTS
+    cap = bn.engine.fused_capacity(target, names, 64)
+    assert cap >= 65536 > cap // 2  # the fused two-round launch
+    out = pdf.cpu().numpy()
+    np.testing.assert_array_equal(dom.cpu().numpy()[:1], z["domain"])
+    two, _ = sharded_infer(bn, target, ev, N_max=64)  # raw launch + scale
+    np.testing.assert_array_equal(two.cpu().numpy(), out)
+    rows, _, words, _ = bn.engine.infer_raw(target, ev, 64)
+    raw = rows.cpu().numpy()
+    gmax = raw.max()
+    assert int(np.argmax(raw.max(1))) == int(z["argmax_row"])
+    r = z["rows"]
+    np.testing.assert_allclose(raw[r], z["raw"], rtol=RTOL, atol=0)
+    assert z["raw"].max() == z["raw"][list(r).index(int(z["argmax_row"]))].max()
+    np.testing.assert_allclose(out[r], z["raw"] / z["raw"].max(), rtol=RTOL, atol=ATOL)
+    assert out.max() == 1.0 and np.isfinite(out).all()
+    assert gmax > 0 and (raw[r] > 0).any(1).mean() > 0.05
 
 
 def test_grid_fast_path_beyond_64_factors(gpu):

@@ -158,8 +158,9 @@ def test_evidence_width_checks_match_reference(name):
     """Evidence columns that are not [Q, 1] (reference fixtures
     err_width*, multi_widthN_partial): InferenceEngine.check_columns raises the
     reference's RuntimeError with its message (node.py:233-234, 246-248) --
-    or NotImplementedError for the [Q, N] column the reference reads as N
-    per-sample values.  Host logic only: the plan's factor specs, no launch."""
+    or returns the [Q, N] columns the reference reads as N per-sample values
+    (the wide direct plan's columns).  Host logic only: the plan's factor
+    specs, no launch."""
     g = load_golden(name)
     m = g["meta"]
     bn = make_bn(BayesianNetwork, m["edges"], m["columns"], g["data"], device="cpu")
@@ -175,8 +176,7 @@ def test_evidence_width_checks_match_reference(name):
             InferenceEngine.check_columns(plan, ev)
         assert str(info.value) == msg
     else:
-        with pytest.raises(NotImplementedError):
-            InferenceEngine.check_columns(plan, ev)
+        assert InferenceEngine.check_columns(plan, ev) == {k for k, v in m["width"].items() if v != 1}
     # the same columns at width 1 pass
-    InferenceEngine.check_columns(plan, {k: v[:, :1] if v.shape[1] else torch.zeros((v.shape[0], 1))
-                                         for k, v in ev.items()})
+    assert InferenceEngine.check_columns(plan, {k: v[:, :1] if v.shape[1] else torch.zeros((v.shape[0], 1))
+                                                for k, v in ev.items()}) == set()

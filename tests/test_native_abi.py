@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     lib = _native.load()
-    assert lib.cbn_abi_version() == 4 == _native.ABI_VERSION
+    assert lib.cbn_abi_version() == 5 == _native.ABI_VERSION
     # cbn_factor_desc: 3 int32 + 2*8 int32 + 3 pointers + 8 pointers (with alignment padding)
     assert ctypes.sizeof(_native.FactorDesc) == 4 * 19 + 4 + 8 * 11
     # cbn_param_model: 8 int32 (family, n_layers, width[5], act) + pointer + 2 float + widths pointer
@@ -36,7 +36,7 @@ def test_abi_version_and_struct_layout():
     # cbn_cpd_ref: n_cols (+4 pad) + 5 pointers + int64
     assert ctypes.sizeof(_native.CpdRef) == 8 + 5 * 8 + 8
     # cbn_direct_factor: 2 int32 + 3 pointers + cpd
-    assert ctypes.sizeof(_native.DirectFactor) == 8 + 3 * 8 + ctypes.sizeof(_native.CpdRef)
+    assert ctypes.sizeof(_native.DirectFactor) == 8 + 3 * 8 + ctypes.sizeof(_native.CpdRef) + 8
 
 
 def test_argument_errors_are_reported_without_gpu():
@@ -195,3 +195,20 @@ def test_runner_key_whose_eq_raises_falls_back():
     r = host.Runner(0, 0, ("a",), ("a",), 0, 4, True, 0, 0, tdom)
     assert r({Key("b"): torch.zeros(8, 1)}, None) is None
     assert r({"a": torch.zeros(8, 1)}, None) is None  # a CPU column: declined too
+
+
+def test_lib_path_override_needs_cbn_diag(monkeypatch):
+    """CBN_LIB_PATH names a diagnostic (unstamped) library build; like the
+    kernel switches it counts only under CBN_DIAG=1 -- a stray variable in a
+    serving process still loads the in-tree, stamp-checked libcbn_amd.so."""
+    default = os.path.join(os.path.dirname(os.path.abspath(_native.__file__)), "libcbn_amd.so")
+    monkeypatch.delenv("CBN_DIAG", raising=False)
+    monkeypatch.setenv("CBN_LIB_PATH", "/tmp/libcbn_amd_stamps.so")
+    assert _native.lib_path() == default
+    monkeypatch.setenv("CBN_DIAG", "0")
+    assert _native.lib_path() == default
+    monkeypatch.setenv("CBN_DIAG", "1")
+    assert _native.lib_path() == "/tmp/libcbn_amd_stamps.so"
+    monkeypatch.delenv("CBN_LIB_PATH")
+    assert _native.lib_path() == default
+    assert _native.LIB_PATH == default  # this process: no override

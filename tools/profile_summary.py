@@ -1,6 +1,6 @@
 """Condense rocprofv3 outputs of a bench run into the files committed under profiles/.
 
-Usage (on the GPU box, after tools/gpu_session.sh prof pmc):
+Usage (on the GPU box, after the prof / fetch / write steps of tools/session.sh):
     python tools/profile_summary.py --tag r01 [--prof gpurun_out/prof]
         [--fetch gpurun_out/pmc_fetch] [--write gpurun_out/pmc_write]
 
