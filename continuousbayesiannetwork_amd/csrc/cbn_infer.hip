@@ -294,13 +294,20 @@ __global__ void k_cpd_scatter(const int32_t* __restrict__ cell, const float* __r
         cpd[cell[r]] = prob[r];  // mle rows are unique -> one writer per cell
 }
 
+// The parent marginal is summed in fp64 and rounded once (round 6): the
+// reference's fp32 sum (torch's cascaded reduction over the unique rows,
+// brute_force.py:236-238) is within a couple of ulp of the exact sum, while a
+// sequential fp32 sum of a peaked row (one dominant joint among 64) drifts by
+// several ulp in a consistent direction -- 3.5e-5 relative over the 100
+// factors of the configs[4] grid at 400 000 training rows
+// (tests/test_gpu_parity.py::test_grid_bench_batch_full_size).  Fit time only.
 __global__ void k_cpd_normalize(float* __restrict__ cpd, long long n_pcells, int card) {
     for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < n_pcells;
          c += (long long)gridDim.x * blockDim.x) {
         float* row = cpd + c * card;
-        float s = 0.f;
-        for (int v = 0; v < card; ++v) s += row[v];
-        const float den = s + 1e-10f;  // brute_force.py:240-241
+        double s = 0.0;
+        for (int v = 0; v < card; ++v) s += (double)row[v];
+        const float den = (float)s + 1e-10f;  // brute_force.py:240-241 (fp32, as the reference)
         for (int v = 0; v < card; ++v) row[v] = row[v] / den;
     }
 }

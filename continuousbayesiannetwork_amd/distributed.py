@@ -235,14 +235,16 @@ def sharded_infer(bn, target_node: str, evidence_shard: Dict[str, torch.Tensor],
 
 def _sharded_on_plan(eng, plan, fp, target_node, evidence_shard, N_max, group, gather, out, multi):
     n = next(iter(evidence_shard.values())).shape[0] if evidence_shard else 1
+    wide = set()
     if n == 0:  # no launch checks an empty shard's columns: raise the reference's shape errors here
-        eng.check_columns(plan, evidence_shard)
+        wide = eng.check_columns(plan, evidence_shard)  # ([Q, N] columns: the wide direct plan's raw launch)
     raw = eng.infer_raw(target_node, evidence_shard, N_max, out, fp=fp) if (fp is not None and n > 0) else None
-    if raw is None and multi and fp is not None and fp.words is not None and n == 0:
+    if raw is None and multi and fp is not None and (fp.words is not None or wide) and n == 0:
         # an empty shard on a raw-capable plan: no rows, zero max words -- the
         # same collectives as the other ranks
         rows = torch.empty((0, plan.n_samples), dtype=torch.float32, device=fp.device)
-        bits = torch.zeros_like(fp.words)
+        bits = (torch.zeros(eng.wide_word_count(plan, wide, fp.device), dtype=torch.int32, device=fp.device)
+                if wide else torch.zeros_like(fp.words))
         raw = (rows, plan.target_domain.unsqueeze(0).expand(0 if plan.target_observed else 1, -1), bits,
                lambda r, b: r)
     # the path must be the same on every rank (different collectives would hang):

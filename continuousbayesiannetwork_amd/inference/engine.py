@@ -795,18 +795,25 @@ class InferenceEngine:
         """
         if fp is None:
             fp = self.raw_fast_path(target, evidence, N_max)
-        if fp is None or fp.words is None:
+        if fp is None:
             return None
+        if fp.words is None:
+            return self._raw_wide(fp, evidence, out)
         plan = fp.plan
         if words is None:
             words = fp.words
         elif (words.dtype is not torch.int32 or words.device != fp.device or words.numel() != fp.words.numel()
               or not words.is_contiguous()):
             raise ValueError(f"words must be a contiguous int32[{fp.words.numel()}] tensor on {fp.device}")
+        built = plan.tables_built
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
                       plan.n_samples, plan.target_observed, words.data_ptr(),
                       self._flags(plan) | _native.CBN_RUN_RAW, out)
         if res is None:  # evidence the native checks reject (dtype, device, layout): convert, launch here
+            plan.tables_built = built  # (nothing launched yet)
+            wres = self._raw_wide(fp, evidence, out)
+            if wres is not None:
+                return wres
             res = self._run_raw_converted(fp, evidence, words, out)
         if res is None or (type(res) is int and res == _native.CBN_E_UNSUPPORTED):
             return None
@@ -833,9 +840,6 @@ class InferenceEngine:
         n = next(iter(evidence.values())).shape[0]
         if n == 0 or (not plan.target_observed and n != 1):
             return None
-        wide = self._wide(plan, evidence)
-        if wide:  # the wide direct plan's raw launch; its max folded into words[0]
-            return self._run_wide(plan, evidence, wide, n, fp.device, out, words=words)
         cols = self._columns(plan, evidence, n, fp.device)
         if out is None:
             out = torch.empty((n, plan.n_samples), dtype=torch.float32, device=fp.device)
@@ -922,9 +926,12 @@ class InferenceEngine:
         """Hot path: no plan lookup, no context managers, no re-validation
         beyond dtype/device/shape of the evidence columns."""
         plan = fp.plan
+        built = plan.tables_built
         res = fp.host(fp.run_fn, plan.handle.value, evidence, fp.slot_keys, fp.first, fp.device.index,
                       plan.n_samples, plan.target_observed, fp.max_ptr, self._flags(plan), out)
-        if res is not None:
+        if res is None:  # nothing launched: the tables are still to be built by the launch that runs
+            plan.tables_built = built
+        else:
             if type(res) is int:
                 _native.check(res, "cbn_plan_run")
             n = res.shape[0]
@@ -1005,10 +1012,10 @@ class InferenceEngine:
         self._wide_plans[key] = (plan, wp)
         return wp
 
-    def _run_wide(self, plan: Plan, evidence, wide, n_queries: int, device, out, words=None):
+    def _run_wide(self, plan: Plan, evidence, wide, n_queries: int, device, out, raw: bool = False):
         """One call with [Q, N] columns on the wide direct plan: raw launch,
-        then (words None) the global-max division; else the launch's max
-        folded into words[0] (the caller's exchange / scale)."""
+        then the global-max division -- or, ``raw``, (rows, target domain, the
+        launch's max words) for the caller's exchange and scale."""
         wp = self._wide_plan(plan, wide, device)
         N = plan.n_samples
         cols = []
@@ -1035,14 +1042,36 @@ class InferenceEngine:
             s = _native.stream_ptr(device)
             _native.check(lib.cbn_plan_run(wp.handle, n_queries, ptrs, len(cols), _native.ptr(wp.words),
                                            _native.ptr(out), flags, s), "cbn_plan_run(wide)")
-            if words is not None:
-                # non-negative floats (NaN propagating, as torch.max): the max of the block words
-                words.zero_()
-                words[:1] = wp.words.view(torch.float32).max().reshape(1).view(torch.int32)
-                return out
+            if raw:
+                return out, tdom, wp.words
             _native.check(lib.cbn_scale(_native.ptr(out), n_queries * N, _native.ptr(wp.words), wp.words.numel(), s),
                           "cbn_scale")
         return out, tdom
+
+    def wide_word_count(self, plan: Plan, wide, device) -> int:
+        """W of the wide direct plan (an empty shard's zero words must match
+        the other ranks' raw launch)."""
+        return int(self._wide_plan(plan, wide, device).words.numel())
+
+    def _raw_wide(self, fp: "_FastPath", evidence, out):
+        """infer_raw of a call with [Q, N] columns: the wide direct plan's raw
+        launch and ITS max words (the same W on every rank, empty shards
+        included: ``wide_word_count``); None for any other call."""
+        n = next(iter(evidence.values())).shape[0] if len(evidence) else 0
+        wide = self._wide(fp.plan, evidence) if n > 0 else None
+        if not wide:
+            return None
+        rows, tdom, words = self._run_wide(fp.plan, evidence, wide, n, fp.device, out, raw=True)
+        return rows, tdom, words, self._wide_scale(fp)
+
+    @staticmethod
+    def _wide_scale(fp: "_FastPath"):
+        def scale(rows: torch.Tensor, bits: torch.Tensor):
+            rc = fp.host_scale(fp.scale_fn, rows, bits.data_ptr(), bits.numel())
+            if rc:
+                _native.check(rc, "cbn_scale")
+            return rows
+        return scale
 
     def _run(self, plan: Plan, evidence, n_queries: int, device, out):
         wide = self._wide(plan, evidence)

@@ -48,9 +48,11 @@ def sparse_conditionals(cell: torch.Tensor, probs: torch.Tensor, card_node: int,
         return probs.clone()
     pcell = torch.div(cell, card_node, rounding_mode="floor")
     _, inv = torch.unique(pcell, return_inverse=True)
-    pmarg = torch.zeros(int(inv.max()) + 1 if inv.numel() else 0, dtype=torch.float32, device=probs.device)
-    pmarg.index_add_(0, inv, probs)
-    return probs / (pmarg[inv] + 1e-10)
+    # summed in fp64 and rounded once (k_cpd_normalize's convention: within an
+    # ulp of the exact marginal, and independent of the atomics' order)
+    pmarg = torch.zeros(int(inv.max()) + 1 if inv.numel() else 0, dtype=torch.float64, device=probs.device)
+    pmarg.index_add_(0, inv, probs.double())
+    return probs / (pmarg.float()[inv] + 1e-10)
 
 
 def hash_capacity(n: int) -> int:
@@ -150,8 +152,10 @@ class BruteForce(BaseParameterLearningEstimator):
                 cell += idx * stride
                 stride *= cards[c]
             # P(node value) over all rows: the query=None case of brute_force.py:192-201
-            marg = torch.zeros(cards[-1], dtype=torch.float32, device=dev)
-            marg.index_add_(0, idx_last, probs)
+            # (fp64, rounded once: see sparse_conditionals)
+            marg = torch.zeros(cards[-1], dtype=torch.float64, device=dev)
+            marg.index_add_(0, idx_last, probs.double())
+            marg = marg.float()
             if n_cells <= self.dense_limit:
                 cell32 = cell.to(torch.int32).contiguous()
                 cpd = torch.empty(n_cells, dtype=torch.float32, device=dev)

@@ -306,6 +306,32 @@ def test_wide_columns_match_oracle(N, Q, gpu):
     np.testing.assert_allclose(pdf1.cpu().numpy(), ref1, rtol=RTOL, atol=ATOL)
     if N <= 4:  # deterministic plans: the pipelined stepper
         st = ShardedStepper(bn, "E", N)
-        with pytest.raises(NotImplementedError):
-            st.step(_t(ev, gpu))
+        if bn.engine.raw_word_count("E", ev.keys(), N) > 0:  # its native ring takes [Q, 1] columns only
+            with pytest.raises(NotImplementedError):
+                st.step(_t(ev, gpu))
+        else:  # no raw launch on the table plan: the stepper serves the call through sharded_infer
+            random.seed(11)
+            rows = st.step(_t(ev, gpu))[0]
+            st.wait()
+            np.testing.assert_allclose(rows.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
         st.close()
+
+
+def test_redrawn_plan_rebuilds_tables_when_host_path_declines(gpu):
+    """A redrawn plan (N = 6 > |domain| = 4: new sample points every call)
+    whose next call's evidence the native host path declines (float64, a
+    [Q, N] column) must still rebuild its tables for that call's draws: the
+    flags computed for a declined host call do not count as a launch."""
+    data, cols, edges = _wide_net()
+    ora = OracleBN(edges, cols, data)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    rng = np.random.default_rng(3)
+    c1 = rng.integers(0, 4, (500, 1)).astype(np.float32)
+    cw = rng.integers(0, 4, (500, 6)).astype(np.float32)
+    for seed, ev, dt in ((21, {"C": c1}, torch.float32), (22, {"C": c1}, torch.float64), (23, {"C": cw}, torch.float32),
+                         (24, {"C": c1}, torch.float32), (25, {"C": c1}, torch.float64)):
+        random.seed(seed)
+        ref, _ = ora.infer("E", ev, 6)
+        random.seed(seed)
+        pdf, _ = bn.infer("E", {k: torch.tensor(v, device=gpu, dtype=dt) for k, v in ev.items()}, N_max=6)
+        np.testing.assert_allclose(pdf.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)

@@ -6,7 +6,7 @@
 #
 # Steps (in the order given; the session stops at the first failure, so a
 # fault or time limit ends it and nothing more touches the GPU):
-#   pytest        the GPU suite (PYTEST_K / PYTEST_FILES narrow it)
+#   pytest        the GPU suite (PYTEST_K / PYTEST_FILES narrow it; PYTEST_X= runs past failures)
 #   smoke         __graft_entry__.smoke()
 #   driverN       the driver's bench command (--gpus 1 --steps 20 --warmup 5), N times
 #   bench         python bench.py (default: 200 steps, the CPU baseline)
@@ -49,7 +49,7 @@ PY
 for step in "$@"; do
   case $step in
     pytest)
-      timeout -k 10 1100 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -q --timeout 300 --timeout-method thread \
+      timeout -k 10 1100 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu ${PYTEST_X--x} -q --timeout 300 --timeout-method thread \
         ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1; rc=$?
       tail -3 $O/pytest_gpu.log
       [ $rc -eq 0 ] || exit $rc ;;
@@ -84,6 +84,7 @@ for step in "$@"; do
       timeout -k 10 120 python3 tools/profile_summary.py --tag "${TAG:-r06}" --prof $O/prof --fetch $O/pmc_fetch \
         --write $O/pmc_write --warmup 5 --steps 20 --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20 --warmup 5 (PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes, --steps 40)" \
         > $O/summary.log 2>&1 || exit $?
+      cp profiles/${TAG:-r06}_summary.json profiles/${TAG:-r06}_kernel_stats.csv $O/  # (gpurun copies gpurun_out back)
       tail -5 $O/summary.log ;;
     pmc*)
       name=${step#pmc}

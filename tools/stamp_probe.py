@@ -6,7 +6,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 import continuousbayesiannetwork_amd._native as nat
-nat.LIB_PATH = os.path.join(ROOT, "continuousbayesiannetwork_amd", "libcbn_amd_stamps.so")
+nat.LIB_PATH = os.environ.get("CBN_LIB_PATH") or os.path.join(ROOT, "continuousbayesiannetwork_amd",
+                                                               "libcbn_amd_stamps.so")
 from continuousbayesiannetwork_amd import BayesianNetwork
 from helpers import chain_data, make_bn, sample_evidence
 
@@ -15,7 +16,6 @@ lib = nat.load()
 lib.cbn_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
 S = 12
 buf = torch.zeros(4096 * 16 * S, dtype=torch.int64, device=dev)
-nat.LIB_PATH = os.environ.get("CBN_LIB_PATH", nat.LIB_PATH)
 if os.environ.get("GRID"):  # BASELINE configs[4]: peaked 10 x 10 grid, k_query_fast on global tables
     from helpers import grid_data
     data, cols, edges = grid_data(400_000, 3, side=10, d=64, keep=0.995, noise=0)
