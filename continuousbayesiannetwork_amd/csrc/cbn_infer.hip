@@ -1444,7 +1444,7 @@ __global__ void __launch_bounds__(kQueryThreads)
 k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, const int* __restrict__ crec,
               FPtrsT<kFastPtrsSmall> sp, long long Q, long long per, int N, int L, unsigned* __restrict__ sync,
               unsigned epoch, const unsigned* __restrict__ max_in, int n_max, unsigned* __restrict__ max_out,
-              float* __restrict__ out, int lds_tab, unsigned long long lmask0, unsigned long long lmask1) {
+              float* __restrict__ out, int lds_tab, unsigned long long lmask0, unsigned long long lmask1, int coal) {
     CBN_STAMP_INIT;
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float* simg = reinterpret_cast<float*>(smem4);
@@ -1503,6 +1503,63 @@ k_query_slots(int nf, int ns, const float* __restrict__ gimage, int qslot_off, c
         const bool valid = qq < q1;
         const long long q = valid ? qq : q0;
         if (first) CBN_STAMP(3);
+        if (coal) {
+            // Index phase, coalesced (round 6): the block round's ns x QB
+            // evidence values as (slot, 4-query) units, one 16-B load each --
+            // a wave reads 1 KB of one or two columns -- mapped to int16
+            // indices in LDS; queries past the batch get -1 (the zero row).
+            // Other waves' queries are written, so a block barrier before
+            // (the previous round's offset reads) and after.
+            if (!first) __syncthreads();
+            const int QB4 = QB >> 2;
+            const int nu = ns * QB4;
+            const long long nv = q1 - qb;  // valid queries of this round
+            constexpr int CU = 4;  // units in flight per lane
+            for (int u0 = 0; u0 < nu; u0 += CU * nthr) {
+                float4 x[CU];
+#pragma unroll
+                for (int k = 0; k < CU; ++k) {
+                    const int u = u0 + k * nthr + tid;
+                    const int uc = u < nu ? u : nu - 1;  // (unconditional loads: counted waits)
+                    const int s = uc / QB4, c4 = (uc - s * QB4) * 4;
+                    const float* src = sptr[s] + qb + c4;
+                    if (c4 + 4 <= nv) {
+                        x[k] = *reinterpret_cast<const float4*>(src);
+                    } else {
+                        x[k].x = c4 + 0 < nv ? src[0] : 0.f;
+                        x[k].y = c4 + 1 < nv ? src[1] : 0.f;
+                        x[k].z = c4 + 2 < nv ? src[2] : 0.f;
+                        x[k].w = c4 + 3 < nv ? src[3] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CU; ++k) {
+                    const int u = u0 + k * nthr + tid;
+                    if (u < nu) {
+                        const int s = u / QB4, c4 = (u - s * QB4) * 4;
+                        const QSlot sr = srec[s];
+                        const float xs[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+                        int iv[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float xv = xs[e];
+                            int i;
+                            if (sr.dense) {
+                                i = (int)xv;
+                                i = (xv >= 0.f && xv < (float)sr.card && (float)i == xv) ? i : -1;
+                            } else {
+                                i = bsearch_eq(gimage + sr.dom_off, sr.card, xv);
+                            }
+                            iv[e] = c4 + e < nv ? i : -1;
+                        }
+                        int* w = reinterpret_cast<int*>(sidx + s * SQ + c4);  // (SQ even, c4 % 4 == 0: 4-B aligned)
+                        w[0] = (iv[0] & 0xFFFF) | (iv[1] << 16);
+                        w[1] = (iv[2] & 0xFFFF) | (iv[3] << 16);
+                    }
+                }
+            }
+            __syncthreads();
+        } else
         for (int c0 = 0; c0 < nsl; c0 += CH) {
             float x[CH];
 #pragma unroll
@@ -2396,10 +2453,24 @@ void launch_fast_k(const cbn_plan* p, unsigned blocks, hipStream_t s, const EvPt
         return;
     }
     if (p->slots) {
+        // Coalesced index phase (round 6: 16-B evidence loads per (slot, 4
+        // queries), the block's waves index every query of the round, block
+        // barriers around it) for launches of >= 3 block rounds: the
+        // configs[4] grid at 262 144 queries 316.5-319.1 -> 279.0-280.1 us,
+        // but at 65 536 (the fused launch's two rounds) 66.2-66.4 -> 73.7-74.1
+        // us -- the barriers put the waves in lockstep across the rounds
+        // (MEASUREMENTS.md, round 6).  Needs 16-B aligned columns and every
+        // block's first query a multiple of 4.
+        const int QBs = kQueryThreads / L;
+        long long per = (Q + blocks - 1) / blocks;
+        int coal = per > 2LL * QBs && !diag_env("CBN_SLOTS_NO_COAL") ? 1 : 0;
+        if (diag_env("CBN_SLOTS_COAL")) coal = 1;
+        for (int i = 0; i < p->ns; ++i) coal &= (reinterpret_cast<uintptr_t>(ev.p[i]) & 15) == 0 ? 1 : 0;
+        if (coal) per = (per + 3) & ~3LL;
         hipLaunchKernelGGL((k_query_slots<VPL, MODE>), dim3(blocks), dim3(kQueryThreads), p->fast_lds_bytes, s, p->nf,
-                           p->ns, p->d_image, p->rec_off + p->nf * kRecFloats, p->d_crec, slot_ptrs(p, ev), Q,
-                           (Q + blocks - 1) / blocks, p->N, L, p->d_sync, epoch, max_in, n_max, max_out, out,
-                           p->lds_tab_floats, p->lds_tab_mask[0], p->lds_tab_mask[1]);
+                           p->ns, p->d_image, p->rec_off + p->nf * kRecFloats, p->d_crec, slot_ptrs(p, ev), Q, per,
+                           p->N, L, p->d_sync, epoch, max_in, n_max, max_out, out, p->lds_tab_floats,
+                           p->lds_tab_mask[0], p->lds_tab_mask[1], coal);
         return;
     }
     if (p->cols) {

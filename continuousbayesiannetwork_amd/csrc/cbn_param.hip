@@ -842,12 +842,16 @@ struct FSplit {
     // lo[p] = 2^-125 G_p and hi[p] = 2^126 / G_p, G_p = the product over part
     // p's factors of max(1, the density's peak) -- an upper bound on any
     // partial product of the range (cbn_param.hip param_split_guard).
-    // gs[p] = 2^-125 prod_{q >= p} G_q bounds both orders' values in a column
-    // where part p's checks fail.  mono: every peak <= 1, so every running
-    // product only falls and the final product alone decides (>= 2^-125).
+    // A column whose checks fail may have rounded in the subnormal range in
+    // either order: each such rounding errs by <= 2^-150 absolute, later
+    // multiplied by at most prod_q G_q, so the orders differ there by <= ucap
+    // = n_factors 2^-148 prod_q G_q beyond their ordinary relative rounding.
+    // mono: every peak <= 1, so every running product only falls and the
+    // final product alone decides (>= 2^-125).
     float lo[7];
     float hi[7];
-    float gs[7];
+    float ucap;
+    float screen;  // 2^-125 G^2 (G = prod_q G_q <= 2^60), else +inf: the exact test runs
     int mono;
 };
 
@@ -860,7 +864,7 @@ struct FSplit {
 #define CBN_WPE_LIN 6  // round 5: 8 -> 6 (80 VGPRs: the column-pair groups of mul_row_t without spills)
 #endif
 #ifndef CBN_WPE_MLP
-#define CBN_WPE_MLP 1
+#define CBN_WPE_MLP 5  // round 6: the order guard's cold tail would take the NN [16] kernel past 102 VGPRs (4 waves)
 #endif
 // M1: every query factor of the plan has all its parents observed (M == 1,
 // e.g. full evidence): the free-combo mean and its TwoSum state (2 x NC
@@ -913,19 +917,14 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[j] = 1.f;  // out_pdf = ones (bayesian_network.py:269)
         float z[kMaxP];
-        // acc *= factors [fb, fe) in order (the reference's running product).
-        // One code site for both passes: the second (the order guard's
-        // continuation, below) re-enters this loop without the barriers.
-        int fb = active ? f0 : f1, fe = f1;  // an idle wave (batch tail) skips its factors
-        bool keep = false;
-        for (bool first = true;; first = false) {
+        const int fa = active ? f0 : f1;  // an idle wave (batch tail) skips its factors
         if constexpr (!(M1 && TAB)) {  // (the M1 table loop loads its own, two factors ahead)
-            if (TAB) load_inputs_tab(ev, fb < nf ? fb : nf - 1, qb, z);
-            else load_inputs(incol + (fb < nf ? fb : nf - 1) * kMaxP, qs, z);
+            if (TAB) load_inputs_tab(ev, fa < nf ? fa : nf - 1, qb, z);
+            else load_inputs(incol + (fa < nf ? fa : nf - 1) * kMaxP, qs, z);
         }
         if constexpr (M1 && TAB) {  // hot headers, one factor ahead
             const PHead* __restrict__ hd = reinterpret_cast<const PHead*>(img + cst_off + 4);
-            PHead h = hd[fb < nf ? fb : nf - 1];
+            PHead h = hd[fa < nf ? fa : nf - 1];
             // Evidence two factors ahead in two buffers used in turn (round
             // 5): no register copy at the end of a factor, and every input
             // is loaded (an input that is not evidence reads the image's 0
@@ -935,7 +934,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
             // factor: the prefetch covered one factor's VALU, not a miss.)
             const float* zcell = img + cst_off;  // {0, 1}: element 0 is 0
             auto load_z = [&](int f, float (&zz)[kMaxP]) {
-                const int fi = f < fe ? f : fe - 1;  // (past the range: reload the last one, unused)
+                const int fi = f < f1 ? f : f1 - 1;  // (past the range: reload the last one, unused)
                 const PEv4 c = reinterpret_cast<const PEv4*>(ev.p)[fi > 0 ? fi : 0];
 #pragma unroll
                 for (int i = 0; i < kTabIn; ++i) zz[i] = gload_b(c.p[i] ? c.p[i] : zcell, c.p[i] ? qb : 0u);
@@ -943,7 +942,7 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 for (int i = kTabIn; i < kMaxP; ++i) zz[i] = 0.f;
             };
             auto eval = [&](int f, const float (&zz)[kMaxP]) {
-                const int fn = f + 1 < fe ? f + 1 : f;
+                const int fn = f + 1 < f1 ? f + 1 : f;
                 const PHead hn = hd[fn];
                 const float* R = img + h.row + col0;
                 if (h.kind != CBN_FACTOR_QUERY) {
@@ -966,21 +965,21 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
                 h = hn;
             };
             float zb[kMaxP];
-            load_z(fb, z);
-            load_z(fb + 1, zb);
-            for (int f = fb; f < fe; f += 2) {
+            load_z(fa, z);
+            load_z(fa + 1, zb);
+            for (int f = fa; f < f1; f += 2) {
                 eval(f, z);
                 load_z(f + 2, z);
-                if (f + 1 < fe) {
+                if (f + 1 < f1) {
                     eval(f + 1, zb);
                     load_z(f + 3, zb);
                 }
             }
         } else
-        for (int f = fb; f < fe; ++f) {
+        for (int f = fa; f < f1; ++f) {
             const PRec& r = rec[f];
             float zn[kMaxP];
-            const int fn = f + 1 < fe ? f + 1 : f;  // next factor's evidence in flight during this one
+            const int fn = f + 1 < f1 ? f + 1 : f;  // next factor's evidence in flight during this one
             if (TAB) load_inputs_tab(ev, fn, qb, zn);
             else load_inputs(incol + fn * kMaxP, qs, zn);
             if (r.kind != CBN_FACTOR_QUERY) {  // query-independent row, built with the plan
@@ -1020,82 +1019,141 @@ k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long l
 #pragma unroll
             for (int i = 0; i < kMaxP; ++i) z[i] = zn[i];
         }
-        if (!first) {
-            if (keep) {  // a lane the guard cleared: its split product, parked in its own slot
-#pragma unroll
-                for (int j = 0; j < NC; ++j) acc[j] = comb[(wid * NC + j) * kWave + lane];
-            }
-            break;
-        }
-        if (parts == 1) break;
-        bool again = false;
-        {
+        if (parts > 1) {
             float* mine = comb + (wid * NC) * kWave + lane;
-            if (part != 0 && active) {
+            if (active) {  // parts 1..: their products; part 0: its own (kept for the order guard)
 #pragma unroll
                 for (int j = 0; j < NC; ++j) mine[j * kWave] = acc[j];
             }
             __syncthreads();
             if (part == 0 && active) {
-                // The parts' products in part order, under the order guard
-                // (FSplit).  Per lane: `must` = the reference's running
-                // product may overflow where the split's does not; U bounds
-                // both orders' values in the columns where some product may
-                // have left the normal range (<= 2^-125 G_p-style bounds:
-                // gs[p] = 2^-125 prod_{q >= p} G_q).  A lane whose U is below
-                // 2^-30 of its own largest product differs by less than
-                // 2^-30 of the global max after the division (that max is at
-                // least this row's) -- it keeps the split's product; any
-                // other lane takes the reference's order: the wave continues
-                // the running product from part 0's range (the reference's
-                // prefix, bit for bit).  The decision is the row's own, so a
-                // row's bits never depend on its wave-mates (sharding).
-                // (Two passes over the LDS products -- the test, then the
-                // same multiplications -- so the test holds no second row of
-                // registers.)
-                bool must = false;
-                float U = 0.f, tmax = 0.f;
+                for (int p = 1; p < parts; ++p) {
 #pragma unroll
-                for (int j = 0; j < NC; ++j) {
-                    float pr = acc[j];
-                    for (int p = 1; p < parts; ++p) {
-                        const float P = mine[(p * NC + j) * kWave];
-                        if (!sp.mono) {
-                            must |= j < ncol && !(pr <= sp.hi[p]);
-                            const float pn = pr * P;
-                            if (j < ncol && (!(P >= sp.lo[p]) || !(pn >= sp.lo[p]))) U = fmaxf(U, sp.gs[p] * fmaxf(1.f, pr));
-                            pr = pn;
-                        } else {
-                            pr = pr * P;
-                        }
-                    }
-                    if (sp.mono && j < ncol && !(pr >= 0x1p-125f)) U = 0x1p-125f;
-                    if (j < ncol) tmax = fmaxf(tmax, pr);
+                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
                 }
-                const bool seq = must || U > tmax * 0x1p-30f;
-                if (__builtin_expect(__any(seq), 0)) {
-                    if (!seq) {
-                        for (int p = 1; p < parts; ++p) {
+                // Order guard (FSplit, round 6).  Screen: every column's
+                // product >= sp.screen = 2^-125 G^2 (G = prod_q G_q <= 2^60)
+                // implies every partial product of either order stayed
+                // normal and finite, so the split equals the reference's
+                // running product to rounding.  A wave with a lane below it
+                // (NaN included) takes the exact test below.
+                bool scr = false;
 #pragma unroll
-                            for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                for (int j = 0; j < NC; ++j) scr |= j < ncol && !(acc[j] >= sp.screen);
+                if (__builtin_expect(__any(scr), 0)) {
+                    // per lane: `must` = the reference's running product may
+                    // overflow where the split's does not; `haz` = some
+                    // column's product may have rounded in the subnormal
+                    // range in one order, where the orders differ by <= ucap
+                    // beyond rounding (FSplit).  A lane whose ucap is below
+                    // 2^-30 of its own largest product differs by less than
+                    // 2^-30 of the global max after the division (that max is
+                    // at least this row's) and keeps the split's product; any
+                    // other failing lane takes the reference's order.  The
+                    // decision is the row's own: its bits never depend on its
+                    // wave-mates (sharding).
+                    bool must = false, haz = false;
+                    float tmax = 0.f;
+#pragma unroll
+                    for (int j = 0; j < NC; ++j) {
+                        if (j < ncol) {
+                            float pr = mine[j * kWave];  // part 0's product: the reference's prefix
+                            if (!sp.mono) {
+                                for (int p = 1; p < parts; ++p) {
+                                    const float P = mine[(p * NC + j) * kWave];
+                                    must |= !(pr <= sp.hi[p]);
+                                    const float pn = pr * P;
+                                    haz |= !(P >= sp.lo[p]) || !(pn >= sp.lo[p]);
+                                    pr = pn;
+                                }
+                            }
+                            haz |= !(acc[j] >= 0x1p-125f);
+                            tmax = fmaxf(tmax, acc[j]);
                         }
-#pragma unroll
-                        for (int j = 0; j < NC; ++j) mine[j * kWave] = acc[j];  // (own slot: free)
                     }
-                    keep = !seq;
-                    fb = sp.f[1];
-                    fe = sp.f[parts];
-                    again = true;
-                } else {
-                    for (int p = 1; p < parts; ++p) {
+                    const bool seq = must || (haz && sp.ucap > tmax * 0x1p-30f);
+                    if (__any(seq)) {
+                        // the reference's order for the `seq` lanes: continue
+                        // the running product from part 0's through factors
+                        // f[1] .. f[parts] (the other lanes park their split
+                        // products in their own slot and take them back)
 #pragma unroll
-                        for (int j = 0; j < NC; ++j) acc[j] = acc[j] * mine[(p * NC + j) * kWave];
+                        for (int j = 0; j < NC; ++j) {
+                            const float p0 = mine[j * kWave];
+                            if (!seq) mine[j * kWave] = acc[j];
+                            acc[j] = seq ? p0 : acc[j];
+                        }
+                        const int ft = sp.f[1], fend = sp.f[parts];
+                        for (int f = ft; f < fend; ++f) {
+                            float zt[kMaxP];
+                            if (TAB) load_inputs_tab(ev, f, qb, zt);
+                            else load_inputs(incol + f * kMaxP, qs, zt);
+                            if constexpr (M1 && TAB) {
+                                const PHead h = reinterpret_cast<const PHead*>(img + cst_off + 4)[f];
+                                const float* R = img + h.row + col0;
+                                if (h.kind != CBN_FACTOR_QUERY) {
+#pragma unroll
+                                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * R[j];
+                                } else {
+                                    float mu;
+                                    if (HMAX == 0 || h.n_layers == 1) {
+                                        mu = lin4(img + h.wp, zt);
+                                    } else {
+                                        const float* PW = img + h.wp;
+                                        switch (h.act) {
+                                            case CBN_ACT_TANH: mu = mlp1p_nin<CBN_ACT_TANH, kTabIn>(PW, h.n_in, h.hid, zt, CBN_ACT_TANH); break;
+                                            case CBN_ACT_RELU: mu = mlp1p_nin<CBN_ACT_RELU, kTabIn>(PW, h.n_in, h.hid, zt, CBN_ACT_RELU); break;
+                                            default: mu = mlp1p_rt(PW, h.n_in, h.hid, zt, h.act); break;
+                                        }
+                                    }
+                                    mul_row_t<NC, MODE < 4 ? MODE : 0>(acc, R, h.scale, h.inv_scale, h.norm, mu);
+                                }
+                            } else {
+                                const PRec& r = rec[f];
+                                if (r.kind != CBN_FACTOR_QUERY) {
+                                    const float* c = img + r.c_off + col0;
+#pragma unroll
+                                    for (int j = 0; j < NC; ++j) acc[j] = acc[j] * c[j];
+                                } else {
+                                    const float* W = img + r.w_off;
+                                    const float* S = img + r.s_off + col0;
+                                    const int mode = mode_of(r.family, r.unit != 0);
+                                    const float sc = r.scale, isc = r.inv_scale, nm = r.norm;
+                                    if (M1 || r.M == 1) {
+                                        mul_row<NC, MODE>(mode, acc, S, sc, isc, nm, query_mu<HMAX, kNMax>(r, img, W, zt, deep));
+                                    } else if constexpr (!M1) {
+                                        float fx[NC], cx[NC];
+#pragma unroll
+                                        for (int j = 0; j < NC; ++j) fx[j] = cx[j] = 0.f;
+                                        const float* FS = img + r.fs_off;
+                                        const int fm = r.free_mask;
+                                        for (int c = 0; c < r.M; ++c) {
+                                            int cc = c;
+#pragma unroll
+                                            for (int i = kMaxP - 1; i >= 0; --i) {
+                                                if (fm & (1 << i)) {
+                                                    const int qd = cc / N;
+                                                    zt[i] = FS[i * N + (cc - qd * N)];
+                                                    cc = qd;
+                                                }
+                                            }
+                                            add_row<NC, MODE>(mode, fx, cx, S, sc, isc, nm, query_mu<HMAX, kNMax>(r, img, W, zt, deep));
+                                        }
+                                        const float Mf = (float)r.M;
+#pragma unroll
+                                        for (int j = 0; j < NC; ++j) acc[j] = acc[j] * ((fx[j] + cx[j]) / Mf);
+                                    }
+                                }
+                            }
+                        }
+                        if (!seq) {
+#pragma unroll
+                            for (int j = 0; j < NC; ++j) acc[j] = mine[j * kWave];
+                        }
                     }
                 }
             }
             __syncthreads();
-        }
-        if (!again) break;
         }
         if (part == 0 && active && valid) {
             float* o = out + q * N + col0;
@@ -1552,7 +1610,7 @@ struct ParamPlan {
     size_t deep_const = 0;  // ... and of the const kernel
     int max_slots = 0;
     int split[7][8] = {};  // factor ranges for 1, 2, 3, 4 and 6 parts (index: parts)
-    float guard_lo[7][8] = {}, guard_hi[7][8] = {}, guard_gs[7][8] = {};  // order guard per split (FSplit)
+    float guard_lo[7][8] = {}, guard_hi[7][8] = {}, guard_ucap[7] = {}, guard_screen[7] = {};  // order guard (FSplit)
     bool guard_ok[7] = {};  // every part's bound G_p <= 2^100 (else the plan runs 1 part)
     bool mono = false;      // every density's peak <= 1
     float* d_image = nullptr;
@@ -1573,12 +1631,14 @@ void launch_query_t(const cbn::ParamPlan* pp, unsigned grid, const PEv& ev, long
     memset(&sp, 0, sizeof(sp));
     sp.parts = parts;
     for (int p = 0; p <= parts; ++p) sp.f[p] = pp->split[parts][p];
+    const bool guard = !diag_env("CBN_PARAM_NO_GUARD");  // (A/B: the split's products kept everywhere)
     for (int p = 0; p < parts; ++p) {
-        sp.lo[p] = pp->guard_lo[parts][p];
-        sp.hi[p] = pp->guard_hi[parts][p];
-        sp.gs[p] = pp->guard_gs[parts][p];
+        sp.lo[p] = guard ? pp->guard_lo[parts][p] : 0.f;
+        sp.hi[p] = guard ? pp->guard_hi[parts][p] : HUGE_VALF;
     }
-    sp.mono = pp->mono ? 1 : 0;
+    sp.ucap = pp->guard_ucap[parts];
+    sp.screen = guard ? pp->guard_screen[parts] : 0.f;
+    sp.mono = pp->mono && guard ? 1 : 0;
     size_t lds = (TAB ? 0 : (size_t)pp->nf * kMaxP * sizeof(InCol)) + pp->deep;
     lds = (lds + 15) & ~(size_t)15;
     sp.comb_off = (int)(lds / sizeof(float));
@@ -1846,9 +1906,12 @@ int create_param_generic(const cbn_param_factor* factors, int n_factors, int N, 
 // max(1, peak_f) bounds every partial product of the range; with G_p <=
 // 2^100 the split is kept and the kernel checks, per lane and column, that
 // the range's product and the reference's running product through part p
-// stayed within [2^-125, 2^126] -- a lane that fails and whose failing
-// columns are not provably below 2^-30 of its own largest value takes the
-// reference's order (the kernel's combine step).
+// stayed within [2^-125, 2^126]; where one may not have, the two orders
+// differ by at most ucap = n_factors 2^-148 prod_q G_q (each subnormal
+// rounding errs by <= 2^-150, then grows by at most the remaining factors'
+// bound) beyond their ordinary relative rounding -- a lane for which that is
+// not below 2^-30 of its own largest value takes the reference's order (the
+// kernel's combine step).
 void param_split_guard(cbn::ParamPlan* pp, const PRec* recs, int n_factors) {
     std::vector<double> peak(n_factors);
     bool mono = true;
@@ -1862,17 +1925,19 @@ void param_split_guard(cbn::ParamPlan* pp, const PRec* recs, int n_factors) {
     for (int parts : {1, 2, 3, 4, 6}) {
         const int* b = pp->split[parts];
         bool ok = true;
-        double Gs = 1.0;  // prod_{q >= p} G_q
-        for (int p = parts - 1; p >= 0; --p) {
+        double Gall = 1.0;  // prod_q G_q
+        for (int p = 0; p < parts; ++p) {
             double G = 1.0;
             for (int f = b[p]; f < b[p + 1]; ++f) G *= std::max(1.0, peak[f]);
             ok = ok && G <= 0x1p100;
-            Gs *= G;
+            Gall *= G;
             pp->guard_lo[parts][p] = ok ? (float)(0x1p-125 * G) : 0.f;
             pp->guard_hi[parts][p] = ok ? (float)(0x1p126 / G) : 0.f;
-            // (beyond the float range: +inf, no lane keeps the split there)
-            pp->guard_gs[parts][p] = 0x1p-125 * Gs <= 0x1p127 ? (float)(0x1p-125 * Gs) : HUGE_VALF;
         }
+        // (beyond the float range: +inf, no hazard lane keeps the split there)
+        const double uc = (double)n_factors * 0x1p-148 * Gall;
+        pp->guard_ucap[parts] = uc <= 0x1p127 ? (float)uc : HUGE_VALF;
+        pp->guard_screen[parts] = Gall <= 0x1p60 ? (float)(0x1p-125 * Gall * Gall) : HUGE_VALF;
         pp->guard_ok[parts] = parts == 1 || ok;
     }
 }

@@ -53,3 +53,31 @@ def test_grid_bench_batch_slots_equals_fast_kernel(gpu):
     res, _ = _child("gridfull", CBN_DIAG="1")
     assert res["diag"] == 1 and res["equal"] and res["nonzero_rows"] > 1000
     assert res["flags"][0] & _native.CBN_PLAN_SLOTS and not res["flags"][1] & _native.CBN_PLAN_SLOTS
+
+
+def test_grid_coalesced_index_phase_equals_per_lane(gpu, tmp_path):
+    """k_query_slots' coalesced index phase (round 6: 16-B evidence loads per
+    (slot, 4 queries), taken by launches of >= 3 block rounds) == the per-lane
+    index phase (CBN_SLOTS_NO_COAL=1 under CBN_DIAG=1) bit for bit on a
+    200 003-query grid batch (the raw launch + scale path, ragged last
+    round), and == the same batch through 4-B-offset column views (the
+    coalesced phase declines unaligned columns); 42 rows vs the oracle."""
+    import random
+
+    import numpy as np
+
+    from helpers import grid_data, sample_evidence
+    from oracle.ref_infer import OracleBN
+
+    outp = str(tmp_path / "rows.npy")
+    res, _ = _child("gridcoal", CBN_DIAG="1", CBN_CHILD_OUT=outp)
+    assert res["diag"] == 1 and res["equal"] and res["equal_unaligned"] and res["nonzero_rows"] > 1000
+    assert all(f & _native.CBN_PLAN_SLOTS for f in res["flags"])
+    data, cols, edges = grid_data(100000, 7, side=5, d=64, keep=0.995, noise=0)
+    target, names = cols[-1], cols[:-1]
+    ev = sample_evidence(data, cols, names, 200003, 3)
+    rows = np.asarray(res["rows"])
+    random.seed(0)
+    ref, _ = OracleBN(edges, cols, data).infer(target, {k: v[rows] for k, v in ev.items()}, 64)
+    got = np.load(outp)
+    np.testing.assert_allclose(got / got.max(), ref, rtol=1e-5, atol=1e-7)
