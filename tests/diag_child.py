@@ -27,32 +27,7 @@ def main(mode: str):
     lib = _native.load()
     res = {"diag": int(lib.cbn_diag_enabled())}
     if mode == "enabled":
-        elif mode == "gridcoal":
-        # >= 3 block rounds (the raw launch + scale path): coalesced index phase
-        # vs the per-lane loads, ragged batch, and a column view that is not
-        # 16-B aligned (the coalesced phase declines it)
-        from helpers import grid_data
-
-        data, cols, edges = grid_data(100000, 7, side=5, d=64, keep=0.995, noise=0)
-        target, names = cols[-1], cols[:-1]
-        ev = {k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, 200003, 3).items()}
-        bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
-        outs = []
-        for no_coal in (False, True):
-            os.environ["CBN_SLOTS_NO_COAL"] = "1" if no_coal else "0"
-            if not no_coal:
-                os.environ.pop("CBN_SLOTS_NO_COAL")
-            outs.append(bn.infer(target, ev, N_max=64)[0].cpu().numpy())
-        off = {k: torch.cat([torch.zeros((1, 1), device=dev), v])[1:] for k, v in ev.items()}  # 4-B offset views
-        outs.append(bn.infer(target, off, N_max=64)[0].cpu().numpy())
-        res["flags"] = [int(lib.cbn_plan_flags(p.handle)) for p in bn.engine._plans.values()]
-        res["equal"] = bool(np.array_equal(outs[0], outs[1], equal_nan=True))
-        res["equal_unaligned"] = bool(np.array_equal(outs[0], outs[2], equal_nan=True))
-        res["nonzero_rows"] = int((outs[0] > 0).any(1).sum())
-        rows = np.append(np.arange(0, 200003, 5003)[:40], [200002, int(np.argmax(outs[0].max(1)))])
-        np.save(os.environ["CBN_CHILD_OUT"], outs[0][rows])
-        res["rows"] = rows.tolist()
-    print(json.dumps(res))
+        print(json.dumps(res))
         return
     import numpy as np
     import torch
@@ -103,6 +78,31 @@ def main(mode: str):
         res["flags"] = flags
         res["equal"] = bool(np.array_equal(outs[0], outs[1], equal_nan=True))
         res["nonzero_rows"] = int((outs[0] > 0).any(1).sum())
+    elif mode == "gridcoal":
+        # >= 3 block rounds (the raw launch + scale path): coalesced index phase
+        # vs the per-lane loads, ragged batch, and a column view that is not
+        # 16-B aligned (the coalesced phase declines it)
+        from helpers import grid_data
+
+        data, cols, edges = grid_data(100000, 7, side=5, d=64, keep=0.995, noise=0)
+        target, names = cols[-1], cols[:-1]
+        ev = {k: torch.tensor(v, device=dev) for k, v in sample_evidence(data, cols, names, 200003, 3).items()}
+        bn = make_bn(BayesianNetwork, edges, cols, data, device=dev)
+        outs = []
+        for no_coal in (False, True):
+            os.environ["CBN_SLOTS_NO_COAL"] = "1" if no_coal else "0"
+            if not no_coal:
+                os.environ.pop("CBN_SLOTS_NO_COAL")
+            outs.append(bn.infer(target, ev, N_max=64)[0].cpu().numpy())
+        off = {k: torch.cat([torch.zeros((1, 1), device=dev), v])[1:] for k, v in ev.items()}  # 4-B offset views
+        outs.append(bn.infer(target, off, N_max=64)[0].cpu().numpy())
+        res["flags"] = [int(lib.cbn_plan_flags(p.handle)) for p in bn.engine._plans.values()]
+        res["equal"] = bool(np.array_equal(outs[0], outs[1], equal_nan=True))
+        res["equal_unaligned"] = bool(np.array_equal(outs[0], outs[2], equal_nan=True))
+        res["nonzero_rows"] = int((outs[0] > 0).any(1).sum())
+        rows = np.append(np.arange(0, 200003, 5003)[:40], [200002, int(np.argmax(outs[0].max(1)))])
+        np.save(os.environ["CBN_CHILD_OUT"], outs[0][rows])
+        res["rows"] = rows.tolist()
     print(json.dumps(res))
 
 

@@ -336,3 +336,37 @@ def test_evidence_width_raises_like_the_reference(gpu):
     # the Node.get_prob mirror raises the same way (node.py:233-234)
     with pytest.raises(RuntimeError):
         bn.nodes_obj["X7"].get_prob({"X6": wide["X6"]}, 8)
+
+
+def test_global_table_plan_with_many_factors_and_few_slots_takes_a_fast_kernel(gpu):
+    """an N = 32 global-table plan (4 lanes per query) with ~100
+    factors and few evidence slots -- the LDS budget for its small tables is
+    sized against the larger of k_query_slots' and k_query_fast's side
+    buffers, so the plan is not dropped to the generic k_query kernel.  A
+    100-node chain d = 32 whose nodes X12, X22, X32 also have X10, X20, X30
+    as parents (three 1 024-row tables: a 400 KB image, beyond LDS), evidence
+    on 6 nodes; the marginals match the oracle."""
+    rng = np.random.default_rng(17)
+    S, d, n = 20000, 32, 100
+    X = np.zeros((S, n), np.int64)
+    X[:, 0] = rng.integers(0, d, S)
+    for i in range(1, n):
+        X[:, i] = (X[:, i - 1] + (rng.random(S) < 0.3) * rng.integers(0, d, S)) % d
+        if i in (12, 22, 32):
+            X[:, i] = (X[:, i - 1] + X[:, i - 2]) % d
+    data = X.astype(np.float32)
+    cols = [f"X{i}" for i in range(n)]
+    edges = [(cols[i - 1], cols[i]) for i in range(1, n)] + [(cols[i - 2], cols[i]) for i in (12, 22, 32)]
+    names = ["X10", "X11", "X20", "X21", "X30", "X31"]
+    ev = sample_evidence(data, cols, names, 3000, 4)
+    bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
+    pdf, _ = bn.infer("X99", {k: torch.tensor(v, device=gpu) for k, v in ev.items()}, N_max=32)
+    fp = bn.engine._fast[("X99", tuple(ev.keys()), 32)]
+    flags = _native.load().cbn_plan_flags(fp.plan.handle)
+    assert flags & (_native.CBN_PLAN_FAST | _native.CBN_PLAN_SLOTS), flags
+    assert not flags & _native.CBN_PLAN_LDS  # a global-table plan
+    sub = np.arange(0, 3000, 97)
+    random.seed(0)
+    ref, _ = OracleBN(edges, cols, data).infer_raw("X99", {k: v[sub] for k, v in ev.items()}, 32)
+    p = pdf.cpu().numpy()[sub]
+    np.testing.assert_allclose(p / p.max(), ref / ref.max(), rtol=1e-5, atol=1e-7)
