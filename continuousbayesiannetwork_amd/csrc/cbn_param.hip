@@ -864,7 +864,14 @@ struct FSplit {
 #define CBN_WPE_LIN 6  // round 5: 8 -> 6 (80 VGPRs: the column-pair groups of mul_row_t without spills)
 #endif
 #ifndef CBN_WPE_MLP
-#define CBN_WPE_MLP 5  // round 6: the order guard's cold tail would take the NN [16] kernel past 102 VGPRs (4 waves)
+// one-hidden-layer M1 kernels of <= 16 columns per lane (configs[3]'s NN
+// [16]): 6 waves per SIMD, 80 VGPRs -- the spills this costs sit in the cold
+// order-guard tail; same box, two rounds, bit-identical rows: 116.5-117.1 ->
+// 114.1-114.2 us at 131 072 queries, 851-852 -> 830-837 us at 1 M (round 6,
+// MEASUREMENTS.md).  32-column kernels: 4 waves (<= 128 VGPRs, round 5's
+// occupancy; at 80 they would spill 130+ registers, unconstrained the cold
+// tail takes them to 152).
+#define CBN_WPE_MLP 6
 #endif
 // M1: every query factor of the plan has all its parents observed (M == 1,
 // e.g. full evidence): the free-combo mean and its TwoSum state (2 x NC
@@ -872,7 +879,7 @@ struct FSplit {
 // budget of the occupancy above.
 template <int NC, int HMAX, int MODE, bool TAB, bool M1>
 __global__ void __launch_bounds__(kQThreads)
-__attribute__((amdgpu_waves_per_eu(!M1 ? 1 : HMAX == 0 ? CBN_WPE_LIN : HMAX == 1 ? CBN_WPE_MLP : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(!M1 ? 1 : HMAX == 0 ? CBN_WPE_LIN : HMAX == 1 ? (NC <= 16 ? CBN_WPE_MLP : 4) : 1, 8)))
 k_param_query(const float* __restrict__ img, int cst_off, int nf, PEv ev, long long Q, int N, int L, int QW,
               int n_words, unsigned* __restrict__ max_out, float* __restrict__ out, FSplit sp) {
     const PRec* __restrict__ rec = reinterpret_cast<const PRec*>(img);

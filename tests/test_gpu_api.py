@@ -345,7 +345,7 @@ def test_global_table_plan_with_many_factors_and_few_slots_takes_a_fast_kernel(g
     buffers, so the plan is not dropped to the generic k_query kernel.  A
     100-node chain d = 32 whose nodes X12, X22, X32 also have X10, X20, X30
     as parents (three 1 024-row tables: a 400 KB image, beyond LDS), evidence
-    on 6 nodes; the marginals match the oracle."""
+    on 7 nodes; the marginals match the oracle."""
     rng = np.random.default_rng(17)
     S, d, n = 20000, 32, 100
     X = np.zeros((S, n), np.int64)
@@ -357,7 +357,7 @@ def test_global_table_plan_with_many_factors_and_few_slots_takes_a_fast_kernel(g
     data = X.astype(np.float32)
     cols = [f"X{i}" for i in range(n)]
     edges = [(cols[i - 1], cols[i]) for i in range(1, n)] + [(cols[i - 2], cols[i]) for i in (12, 22, 32)]
-    names = ["X10", "X11", "X20", "X21", "X30", "X31"]
+    names = ["X10", "X11", "X20", "X21", "X30", "X31", "X98"]  # (X98: the target needs an observed parent)
     ev = sample_evidence(data, cols, names, 3000, 4)
     bn = make_bn(BayesianNetwork, edges, cols, data, device=gpu)
     pdf, _ = bn.infer("X99", {k: torch.tensor(v, device=gpu) for k, v in ev.items()}, N_max=32)
