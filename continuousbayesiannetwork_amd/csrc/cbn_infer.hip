@@ -2271,38 +2271,89 @@ k_query_staged(const float* __restrict__ gimage, int image_floats, int rec_off, 
     }
 }
 
-// out[i] /= max (bayesian_network.py:296) after a raw launch and the
-// cross-rank all-reduce of the max word; float4 stream, grid-stride.
-__global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_in,
-                                               int n_max, unsigned* __restrict__ pub) {
-    unsigned mb = 0;  // every wave reduces the (all-reduced) per-block maxima itself
-    for (int i = threadIdx.x & (kWave - 1); i < n_max; i += kWave) mb = max(mb, max_in[i]);
-    mb = wave_max_u(mb);
-    if (pub && blockIdx.x == 0 && threadIdx.x == 0) *pub = mb;
-    const float m = __uint_as_float(mb);
+// max of the n per-block max words, in every lane of the wave.  Every wave of
+// a scale launch needs it, and the words were written by other XCDs' blocks
+// (an L2 miss each): 16 coalesced loads in flight per lane, so the common
+// word counts (256 .. 1 024) cost one round trip instead of n / 64.
+__device__ __forceinline__ unsigned max_words(const unsigned* __restrict__ w, int n) {
+    const int lane = threadIdx.x & (kWave - 1);
+    unsigned m = 0;
+    int i = lane;
+    for (; i + 15 * kWave < n; i += 16 * kWave) {
+        unsigned t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t[k] = w[i + k * kWave];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) m = max(m, t[k]);
+    }
+    for (; i + 3 * kWave < n; i += 4 * kWave) {
+        unsigned t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = w[i + k * kWave];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m = max(m, t[k]);
+    }
+    for (; i < n; i += kWave) m = max(m, w[i]);
+    return wave_max_u(m);
+}
+
+__device__ __forceinline__ float4 div4(float4 v, float m) {
+    v.x = v.x / m;
+    v.y = v.y / m;
+    v.z = v.z / m;
+    v.w = v.w / m;
+    return v;
+}
+
+// out[0, n) /= max(max_in[0, n_max)) over a grid-stride float4 stream, U
+// float4 per thread in flight; the thread's first U are loaded before the max
+// words, so the two round trips overlap.
+template <int U>
+__device__ __forceinline__ void scale_stream(float* __restrict__ out, long long n, const unsigned* __restrict__ max_in,
+                                             int n_max, unsigned* __restrict__ pub) {
     const long long n4 = n / 4;
     float4* o4 = reinterpret_cast<float4*>(out);
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 v = o4[i];
-        v.x = v.x / m;
-        v.y = v.y / m;
-        v.z = v.z / m;
-        v.w = v.w / m;
-        o4[i] = v;
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + u * stride < n4) v[u] = o4[i + u * stride];
+    const unsigned mb = max_words(max_in, n_max);
+    if (pub && blockIdx.x == 0 && threadIdx.x == 0) *pub = mb;
+    const float m = __uint_as_float(mb);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + u * stride < n4) o4[i + u * stride] = div4(v[u], m);
+    i += U * stride;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = o4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) o4[i + u * stride] = div4(v[u], m);
     }
-    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
-        out[i] = out[i] / m;
+    for (; i < n4; i += stride) o4[i] = div4(o4[i], m);
+    for (long long j = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += stride)
+        out[j] = out[j] / m;
+}
+
+// out[i] /= max (bayesian_network.py:296) after a raw launch and the
+// cross-rank all-reduce of the max word; one float4 per thread in flight
+// streams faster here than 8 (23 vs 32 us over 134 MB, session r06t) on the
+// full grid launch_scale gives it.
+__global__ void __launch_bounds__(256) k_scale(float* __restrict__ out, long long n, const unsigned* __restrict__ max_in,
+                                               int n_max, unsigned* __restrict__ pub) {
+    scale_stream<1>(out, n, max_in, n_max, pub);
 }
 
 // k_scale over up to kScaleBatch (out, n) pairs in one launch (blockIdx.y =
 // pair b, dividing by the max of max_in[b * n_max, (b + 1) * n_max)): the
-// pipelined sharded stepper exchanges and scales several steps at once.
+// pipelined sharded stepper exchanges and scales several steps at once; a
+// small grid (it runs beside the next steps' raw launches on the comm stream,
+// in the wave slots those leave free) still streams at HBM rate with
+// kScaleU float4 per thread in flight.
 constexpr int kScaleBatch = 8;
-#ifndef CBN_SCALE_U
-#define CBN_SCALE_U 8
-#endif
-constexpr int kScaleU = CBN_SCALE_U;
+constexpr int kScaleU = 8;
 struct ScaleBatch {
     float* out[kScaleBatch];
     long long n[kScaleBatch];
@@ -2310,45 +2361,7 @@ struct ScaleBatch {
 
 __global__ void __launch_bounds__(256) k_scale_batch(ScaleBatch sb, const unsigned* __restrict__ max_in, int n_max) {
     const int b = blockIdx.y;
-    float* __restrict__ out = sb.out[b];
-    const long long n = sb.n[b];
-    const unsigned* mi = max_in + (long long)b * n_max;
-    unsigned mb = 0;
-    for (int i = threadIdx.x & (kWave - 1); i < n_max; i += kWave) mb = max(mb, mi[i]);
-    mb = wave_max_u(mb);
-    const float m = __uint_as_float(mb);
-    const long long n4 = n / 4;
-    float4* o4 = reinterpret_cast<float4*>(out);
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    // kScaleU float4 per thread in flight: a small grid (it runs beside the
-    // next steps' raw launches on the comm stream, in the wave slots those
-    // leave free) still streams at HBM rate
-    constexpr int U = kScaleU;
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    for (; i + (U - 1) * stride < n4; i += U * stride) {
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = o4[i + u * stride];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v[u].x = v[u].x / m;
-            v[u].y = v[u].y / m;
-            v[u].z = v[u].z / m;
-            v[u].w = v[u].w / m;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) o4[i + u * stride] = v[u];
-    }
-    for (; i < n4; i += stride) {
-        float4 v = o4[i];
-        v.x = v.x / m;
-        v.y = v.y / m;
-        v.z = v.z / m;
-        v.w = v.w / m;
-        o4[i] = v;
-    }
-    for (long long j = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n; j += stride)
-        out[j] = out[j] / m;
+    scale_stream<kScaleU>(sb.out[b], sb.n[b], max_in + (long long)b * n_max, n_max, nullptr);
 }
 
 // *out = max of n words (public query_max: per-block maxima -> one word)
@@ -2375,8 +2388,13 @@ int cbn::num_cu() {
 }
 
 int cbn::launch_scale(float* out, long long n, const unsigned* words, int n_words, unsigned* pub, hipStream_t s) {
+    static const int per_cu = [] {  // blocks per CU at most (diagnostic: CBN_SCALE_CAP)
+        const char* e = diag_env("CBN_SCALE_CAP");
+        const int x = e ? atoi(e) : 0;
+        return x >= 1 && x <= 32 ? x : 4;
+    }();
     long long blocks = (n / 4 + 255) / 256;
-    const long long cap = 4LL * num_cu();
+    const long long cap = (long long)per_cu * num_cu();
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, s, out, n, words, n_words, pub);
